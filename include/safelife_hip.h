@@ -1,0 +1,188 @@
+/*
+ * safelife_hip.h -- C ABI of the MI355X (gfx950) SafeLife stepper.
+ *
+ * Plain pointers and sizes only; every pointer argument marked "dev" is device
+ * memory on the current HIP device, every call is stream-ordered on `stream`
+ * (a hipStream_t passed as void*, NULL = default stream) and returns 0 or a
+ * negative SL_E* code.  No global state: two streams may run independent
+ * batches concurrently.  Layouts are row-major uint16 [B, H, W] boards
+ * (bit layout of safelife_game.py:74-120 / speedups_src/constants.h:4-25).
+ *
+ * Reference interfaces each entry point replaces:
+ *   sl_advance          speedups.advance_board(board, spawn_prob=0.3)
+ *                       /root/reference/safelife/speedups_src/module.c:19-44
+ *                       (batched over B boards; the reference does one per call)
+ *   sl_count_eligible   the draw count of one advance_board call
+ *                       (random_float() calls, advance_board.c:110) -- used to
+ *                       place each board's draws in the reference stream
+ *                       (speedups.seed / random.c:28-52)
+ *   sl_env_step         SafeLifeEnv.step (safelife_env.py:157-186) under the
+ *                       PPO chain MovementBonusWrapper -> SimpleSideEffectPenalty
+ *                       -> ContinuingEnv (training/safelife_ppo.py:128-139,
+ *                       env_wrappers.py:67-88,319-346,298-303) for B envs at once,
+ *                       as driven by PPO.run_agents (training/ppo.py:436-452)
+ *   sl_env_reset        SafeLifeEnv.reset (safelife_env.py:188-198) + the
+ *                       wrappers' resets (env_wrappers.py:90-94,313-317) for the
+ *                       envs selected by a mask, from a device level pool
+ *                       (the level_iterator / safelife_loader contract,
+ *                       file_finder.py:143-201)
+ *   sl_env_obs          SafeLifeEnv.get_obs (safelife_env.py:125-155) +
+ *                       recenter_view (helper_utils.py:41-74)
+ */
+#ifndef SAFELIFE_HIP_H
+#define SAFELIFE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SL_OK 0
+#define SL_EINVAL (-1)      /* bad shape or argument */
+#define SL_EHIP (-2)        /* HIP runtime / launch error */
+#define SL_ETOOBIG (-3)     /* board too large for the selected kernel */
+
+#define SL_RNG_STREAM 0     /* replay a supplied uniform stream (reference order) */
+#define SL_RNG_PHILOX 1     /* counter-based Philox4x32-10 (production) */
+
+#define SL_MAX_EXITS 8      /* exits tracked per env (benchmark levels have 1) */
+#define SL_BONUS_PERIOD_MAX 16
+
+#define SL_OBS_NONE 0
+#define SL_OBS_PACKED 1     /* uint16 [B, vh, vw]           (output_channels=None) */
+#define SL_OBS_CHANNELS 2   /* uint16 [B, vh, vw, nch]      (output_channels=(...)) */
+#define SL_OBS_CHANNELS_U8 3 /* uint8 [B, vh, vw, nch]      (same values, 1 byte)  */
+
+/* Library / device info. */
+const char *sl_version(void);
+int sl_device_arch(char *buf, int len);   /* e.g. "gfx950" */
+
+/* ---------------------------------------------------------------- boards -- */
+
+/*
+ * Advance B independent boards one step: out[b] = rule(in[b]).
+ *   in, out      dev uint16 [B,H,W]; must not alias.  H, W >= 2.
+ *   spawn_prob   dev float [B] or NULL (then spawn_prob_scalar for all boards);
+ *                each draw u spawns iff u < (double)spawn_prob (a C float, as
+ *                the reference parses it with format "f", module.c:22-24).
+ *   rng_mode     SL_RNG_STREAM: board b consumes draws[draw_offsets[b] + k] for
+ *                its k-th eligible cell in row-major order (draws/draw_offsets
+ *                may be NULL when no board can draw: p <= 0 or p >= 1 decide
+ *                without a draw).  SL_RNG_PHILOX: u = philox(seed; cell, env0+b,
+ *                step, tensor).
+ */
+int sl_advance(const uint16_t *in, uint16_t *out, int64_t B, int H, int W,
+               const float *spawn_prob, float spawn_prob_scalar, int rng_mode,
+               uint64_t seed, uint32_t env0, uint32_t step, uint32_t tensor,
+               const double *draws, const int64_t *draw_offsets, void *stream);
+
+/* counts[b] = number of uniform draws board b consumes in one advance. */
+int sl_count_eligible(const uint16_t *in, int64_t *counts, int64_t B, int H, int W,
+                      void *stream);
+
+/* out[i] = base + sum_{j<i} in[j]; *total_out (dev, may be NULL) = base + sum. */
+int sl_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n,
+                          const int64_t *base, int64_t *total_out, void *stream);
+
+/* ------------------------------------------------------------------ envs -- */
+
+/* Per-env state, structure of arrays, all dev pointers, length B unless noted. */
+typedef struct sl_env_state {
+    int64_t B;
+    int32_t H, W;
+    uint16_t *board;          /* [B,H,W]  game.board                          */
+    uint16_t *goals;          /* [B,H,W]  game.goals                          */
+    uint16_t *start_board;    /* [B,H,W]  game._init_data['board']            */
+    int32_t *agent_x, *agent_y, *orientation;
+    int32_t *game_over;
+    int32_t *episode_length;
+    int32_t *episode_reward;  /* SafeLifeEnv's own (integer) reward sum       */
+    int32_t *old_points;      /* SafeLifeEnv._old_game_value                  */
+    int32_t *baseline;        /* perf baseline over _init_data (per episode)  */
+    int32_t *score;           /* current perf score (unit rewards)            */
+    int32_t *possible;        /* perf possible score                          */
+    int32_t *side_effect;     /* SimpleSideEffectPenalty.last_side_effect     */
+    float *spawn_prob;
+    double *min_performance;  /* game.min_performance                         */
+    int32_t *prior_x;         /* [B, SL_BONUS_PERIOD_MAX] position ring        */
+    int32_t *prior_y;
+    int32_t *prior_len;       /* entries in the ring (deque length)           */
+    int32_t *prior_head;      /* index of the oldest entry                    */
+    int32_t *exit_count;
+    int16_t *exit_y, *exit_x; /* [B, SL_MAX_EXITS], np.nonzero order          */
+    int32_t *level_index;     /* level of the current episode                 */
+    int32_t *episodes;        /* episodes started by this env                 */
+    int32_t *num_steps;       /* game.num_steps                               */
+} sl_env_state;
+
+/* A device-resident level pool (the level_iterator's levels). */
+typedef struct sl_level_pool {
+    int32_t K, H, W;
+    const uint16_t *board;    /* [K,H,W] as stored (exits uncoloured)         */
+    const uint16_t *goals;    /* [K,H,W]                                      */
+    const int32_t *agent_x, *agent_y, *orientation;
+    const float *spawn_prob;
+    const double *min_performance;  /* the level's own value (used for the
+                                       reset-time exit colour only)           */
+} sl_level_pool;
+
+typedef struct sl_env_cfg {
+    int32_t time_limit;             /* SafeLifeEnv.time_limit (1000)          */
+    int32_t auto_reset;             /* 1: ContinuingEnv + caller reset-on-done */
+    int32_t can_toggle_powers, can_toggle_colors;
+    double penalty_coef;            /* SimpleSideEffectPenalty (scheduled)    */
+    double wrapper_min_performance; /* SimpleSideEffectPenalty.min_performance;
+                                       applied at reset (NaN = keep level's)  */
+    const double *bonus_table;      /* dev [bonus_len]: movement_bonus *
+                                       (d/period)**power for integer d        */
+    int32_t bonus_len;
+    int32_t bonus_period;           /* movement_bonus_period (<= 16; 0 = off) */
+    int32_t rng_mode;               /* SL_RNG_*                               */
+    uint64_t seed;
+    uint32_t step;                  /* batched-step index (Philox counter)     */
+    uint32_t env0;                  /* global id of env 0 (multi-GPU shards)   */
+    const double *draws;            /* SL_RNG_STREAM: dev uniform stream       */
+    int64_t n_draws;
+    int64_t *stream_pos;            /* dev [1]: next unread draw (advanced)    */
+    int64_t *scratch;               /* dev [5*B + 16] workspace               */
+    int32_t level_mode;             /* 0: level = (env0+b + episodes*n_total)%K,
+                                       1: Philox-random level                  */
+    int32_t n_total_envs;           /* envs across all shards                  */
+    int32_t augment_roll;           /* 1: random toroidal roll per episode     */
+} sl_env_cfg;
+
+/*
+ * One env-step for all B envs (in place on `st`).
+ *   actions     dev int32 [B], 0..8 (safelife_env.py:61-71)
+ *   reward      dev double [B]      chain reward (float64, as Python computes it)
+ *   done        dev uint8 [B]       done as returned to the caller (times_up)
+ *   info_flags  dev uint8 [B] or NULL: bit0 times_up, bit1 game_over,
+ *               bit2 env was reset this step
+ *   ep_len, ep_reward  dev int32 [B] or NULL: finished-episode length / reward
+ * With cfg->auto_reset the done/game-over envs are reset from `pool` before
+ * returning (so the next sl_env_obs sees the new episode).
+ */
+int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const int32_t *actions,
+                const sl_env_cfg *cfg, double *reward, uint8_t *done,
+                uint8_t *info_flags, int32_t *ep_len, int32_t *ep_reward,
+                void *stream);
+
+/* Reset the envs with mask[b] != 0 (mask NULL = all) from `pool`. */
+int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const uint8_t *mask,
+                 const sl_env_cfg *cfg, void *stream);
+
+/*
+ * Observations centred on each agent.
+ *   obs_mode SL_OBS_PACKED: out uint16 [B,vh,vw]; SL_OBS_CHANNELS: uint16
+ *   [B,vh,vw,nch] with channel k = bit channels[k]; SL_OBS_CHANNELS_U8: uint8.
+ *   channels: host int array [nch] (<= 16) -- copied into kernel arguments.
+ */
+int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_white_goals,
+               int obs_mode, const int32_t *channels, int nch, void *out,
+               void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAFELIFE_HIP_H */

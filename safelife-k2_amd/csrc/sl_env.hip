@@ -1,0 +1,667 @@
+// sl_env.hip -- batched SafeLife env step / reset / observation for gfx950.
+//
+// One env-step of the PPO chain, for B envs held as uint16 [B,H,W] device boards:
+//   k_env_action      execute_action / move_agent / relative_loc
+//                     (safelife_game.py:294-393), one lane per env
+//   k_env_count       replay mode only: draws each board will consume
+//   k_env_step_generic  advance board+goals (safelife_game.py:657-660), points
+//                     (:590-599), performance ratio (:601-631), exit colours
+//                     (:528-537), SafeLifeEnv.step bookkeeping (safelife_env.py:
+//                     157-186), MovementBonusWrapper (env_wrappers.py:67-88) and
+//                     SimpleSideEffectPenalty (env_wrappers.py:319-346); one
+//                     workgroup per env, board+goals staged in LDS
+//   k_env_reset       SafeLifeEnv.reset + wrapper resets from a level pool
+//   k_env_obs         get_obs + recenter_view (safelife_env.py:125-155,
+//                     helper_utils.py:41-74)
+#include "sl_device.h"
+#include "../../include/safelife_hip.h"
+
+#include <math.h>
+
+using namespace sl;
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int kMaxCells = 16384;          // board+goals in LDS: 64 KiB
+
+// scratch layout (int64 words)
+//   [0, 2B)   per-(env, tensor) draw counts      (replay mode)
+//   [2B, 4B)  per-(env, tensor) stream offsets   (replay mode)
+//   [4B, 5B)  action reward (int32 stored in int64)
+//   [5B]      error flags (bit0: draw stream exhausted)
+struct Scratch {
+    int64_t *counts, *offsets, *act_reward, *err;
+};
+__host__ __device__ inline Scratch scratch_of(int64_t *s, int64_t B) {
+    return Scratch{s, s + 2 * B, s + 4 * B, s + 5 * B};
+}
+
+__device__ __forceinline__ int pymod(int a, int m) {
+    int r = a % m;
+    return r < 0 ? r + m : r;
+}
+
+__device__ __forceinline__ void forward_vec(int orientation, int *fx, int *fy) {
+    // relative_loc(n_forward=1): dx=0, dy=-1 rotated clockwise `orientation` times
+    int dx = 0, dy = -1;
+    for (int k = 0; k < (orientation & 3); k++) {
+        int t = dx;
+        dx = -dy;
+        dy = t;
+    }
+    *fx = dx;
+    *fy = dy;
+}
+
+__device__ __forceinline__ bool can_exit_now(double mp, int score, int baseline, int possible) {
+    if (mp < 0.0) return true;
+    return (double)(score - baseline) >= mp * (double)(possible - baseline);
+}
+
+// ---------------------------------------------------------------------------
+// actions: one lane per env (cells touched: agent, front, behind, 2 ahead)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int ctc,
+             int64_t *__restrict__ act_reward) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= st.B) return;
+    const int H = st.H, W = st.W;
+    uint16_t *bd = st.board + b * (int64_t)H * W;
+    int reward = 0;
+    const int a = actions[b];
+    if (!st.game_over[b] && a >= 1 && a <= 8) {
+        const int orient = (a - 1) & 3;
+        st.orientation[b] = orient;
+        int fx, fy;
+        forward_vec(orient, &fx, &fy);
+        const int x0 = st.agent_x[b], y0 = st.agent_y[b];
+        const int x1 = pymod(x0 + fx, W), y1 = pymod(y0 + fy, H);
+        if (a <= 4) {
+            // move_agent(1)
+            const int x2 = pymod(x0 - fx, W), y2 = pymod(y0 - fy, H);
+            int nx = x0, ny = y0;
+            uint32_t c1 = bd[y1 * W + x1];
+            if (c1 == 0) {
+                bd[y1 * W + x1] = bd[y0 * W + x0];
+                bd[y0 * W + x0] = 0;
+                nx = x1; ny = y1;
+            } else if ((c1 & EXIT) &&
+                       can_exit_now(st.min_performance[b], st.score[b], st.baseline[b],
+                                    st.possible[b])) {
+                st.game_over[b] = 1;
+                reward += 1;
+            } else if (c1 & PUSHABLE) {
+                const int x3 = pymod(x0 + 2 * fx, W), y3 = pymod(y0 + 2 * fy, H);
+                uint32_t c3 = bd[y3 * W + x3];
+                if (c3 == 0) {
+                    bd[y3 * W + x3] = bd[y1 * W + x1];
+                    bd[y1 * W + x1] = bd[y0 * W + x0];
+                    bd[y0 * W + x0] = 0;
+                    nx = x1; ny = y1;
+                } else if (c3 & EXIT) {
+                    bd[y1 * W + x1] = bd[y0 * W + x0];
+                    bd[y0 * W + x0] = 0;
+                    nx = x1; ny = y1;
+                }
+            }
+            const bool moved = (nx == x1 && ny == y1) && !(x0 == x1 && y0 == y1);
+            if (moved && (bd[y2 * W + x2] & PULLABLE)) {
+                bd[y0 * W + x0] = bd[y2 * W + x2];
+                bd[y2 * W + x2] = 0;
+            }
+            st.agent_x[b] = nx;
+            st.agent_y[b] = ny;
+        } else {
+            // TOGGLE
+            const uint32_t pc = bd[y0 * W + x0] & COLORS;
+            const uint32_t t = bd[y1 * W + x1];
+            if (t == 0) {
+                bd[y1 * W + x1] = (uint16_t)(LIFE | pc);
+            } else if (t & DESTR) {
+                bd[y1 * W + x1] = 0;
+            } else {
+                uint32_t tb = (ctp ? POWERS : 0u) | (ctc ? COLORS : 0u);
+                bd[y0 * W + x0] = (uint16_t)(bd[y0 * W + x0] ^ (t & tb));
+            }
+        }
+    }
+    act_reward[b] = reward;
+}
+
+// ---------------------------------------------------------------------------
+// shared block pieces
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void stage(uint16_t *dst, const uint16_t *src, int hw) {
+    if ((((uintptr_t)src) & 15) == 0 && (hw & 7) == 0) {
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+        for (int i = threadIdx.x; i < (hw >> 3); i += NT) d4[i] = s4[i];
+    } else {
+        for (int i = threadIdx.x; i < hw; i += NT) dst[i] = src[i];
+    }
+}
+
+__device__ __forceinline__ int block_rank(bool flag, int *wave_tot, int *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long m = __ballot(flag);
+    int below = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_tot[wid] = __popcll(m);
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+        int t = wave_tot[w];
+        off += (w < wid) ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + below;
+}
+
+// reduce 4 ints over the block; result valid in thread 0
+__device__ __forceinline__ void block_sum4(int v[4], int (*red)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = wave_sum(v[k]);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0)
+        for (int k = 0; k < 4; k++) red[wid][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 4; k++) {
+            int t = 0;
+            for (int w = 0; w < NT / 64; w++) t += red[w][k];
+            v[k] = t;
+        }
+}
+
+__global__ void __launch_bounds__(NT)
+k_env_count(sl_env_state st, int64_t *__restrict__ counts) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    __shared__ int red[NT / 64][4];
+    const int H = st.H, W = st.W, hw = H * W;
+    const int64_t b = blockIdx.x;
+    uint16_t *lb = lds, *lg = lds + hw;
+    stage(lb, st.board + b * hw, hw);
+    stage(lg, st.goals + b * hw, hw);
+    __syncthreads();
+    int v[4] = {0, 0, 0, 0};
+    for (int i = threadIdx.x; i < hw; i += NT) {
+        const int y = i / W, x = i - y * W;
+        bool e;
+        uint32_t sv;
+        rule_cell(lb[i], gather_lds(lb, H, W, y, x), &e, &sv);
+        v[0] += e;
+        rule_cell(lg[i], gather_lds(lg, H, W, y, x), &e, &sv);
+        v[1] += e;
+    }
+    block_sum4(v, red);
+    if (threadIdx.x == 0) {
+        counts[2 * b] = v[0];
+        counts[2 * b + 1] = v[1];
+    }
+}
+
+struct StepArgs {
+    int32_t time_limit, auto_reset, bonus_len, bonus_period;
+    double penalty_coef;
+    const double *bonus_table;
+    uint64_t seed;
+    uint32_t step, env0;
+    const double *draws;
+    int64_t n_draws;
+};
+
+template <int RNG>
+__global__ void __launch_bounds__(NT)
+k_env_step_generic(sl_env_state st, StepArgs a, const int64_t *__restrict__ act_reward,
+                   const int64_t *__restrict__ offsets, int64_t *__restrict__ err,
+                   double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
+                   uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
+                   int32_t *__restrict__ ep_rew_out) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    __shared__ int red[NT / 64][4];
+    __shared__ int wave_tot[NT / 64];
+    const int H = st.H, W = st.W, hw = H * W;
+    const int64_t b = blockIdx.x;
+    uint16_t *lb = lds, *lg = lds + hw;
+    uint16_t *gb = st.board + b * hw, *gg = st.goals + b * hw;
+    const uint16_t *gs = st.start_board + b * hw;
+    stage(lb, gb, hw);
+    stage(lg, gg, hw);
+    __syncthreads();
+
+    const double thr = (double)st.spawn_prob[b];
+    int64_t pos_b = 0, pos_g = 0;
+    if (RNG == SL_RNG_STREAM) {
+        pos_b = offsets[2 * b];
+        pos_g = offsets[2 * b + 1];
+    }
+    int acc[4] = {0, 0, 0, 0};   // points, score, possible, side effects
+    const int nchunk = (hw + NT - 1) / NT;
+    for (int c = 0; c < nchunk; c++) {
+        const int i = c * NT + threadIdx.x;
+        uint32_t vb = 0, vg = 0, nb = 0, ng = 0, sb = 0, sg = 0;
+        bool eb = false, eg = false;
+        if (i < hw) {
+            const int y = i / W, x = i - y * W;
+            vb = lb[i];
+            vg = lg[i];
+            nb = rule_cell(vb, gather_lds(lb, H, W, y, x), &eb, &sb);
+            ng = rule_cell(vg, gather_lds(lg, H, W, y, x), &eg, &sg);
+        }
+        double ub = 1.0, ug = 1.0;
+        if (RNG == SL_RNG_STREAM) {
+            int tb, tg;
+            const int rb = block_rank(eb, wave_tot, &tb);
+            const int rg = block_rank(eg, wave_tot, &tg);
+            if (eb) {
+                if (thr <= 0.0) ub = 1.0;
+                else if (thr >= 1.0) ub = 0.0;
+                else if (pos_b + rb < a.n_draws) ub = a.draws[pos_b + rb];
+                else atomicOr((unsigned long long *)err, 1ull);
+            }
+            if (eg) {
+                if (thr <= 0.0) ug = 1.0;
+                else if (thr >= 1.0) ug = 0.0;
+                else if (pos_g + rg < a.n_draws) ug = a.draws[pos_g + rg];
+                else atomicOr((unsigned long long *)err, 1ull);
+            }
+            pos_b += tb;
+            pos_g += tg;
+        } else {
+            if (eb) ub = philox_uniform((uint32_t)i, a.env0 + (uint32_t)b, a.step, 0u, a.seed);
+            if (eg) ug = philox_uniform((uint32_t)i, a.env0 + (uint32_t)b, a.step, 1u, a.seed);
+        }
+        if (eb && ub < thr) nb = sb;
+        if (eg && ug < thr) ng = sg;
+        if (i < hw) {
+            const uint32_t s = gs[i];
+            int p, q, r;
+            cell_scores(nb, ng, &p, &q, &r);
+            acc[0] += p;
+            acc[1] += q;
+            acc[2] += r;
+            acc[3] += side_term(nb, s, ng);
+            gg[i] = (uint16_t)ng;
+            if (!(s & EXIT)) gb[i] = (uint16_t)nb;   // exits: recoloured below
+        }
+    }
+    block_sum4(acc, red);
+    if (threadIdx.x != 0) return;
+
+    // ---- per-env epilogue (SafeLifeEnv.step + wrappers) ----
+    const int points = acc[0], score = acc[1], possible = acc[2], side = acc[3];
+    const int r_int = (int)act_reward[b] + (points - st.old_points[b]);
+    st.old_points[b] = points;
+    st.num_steps[b] += 1;
+    const int ep_len = st.episode_length[b] + 1;
+    const int ep_rew = st.episode_reward[b] + r_int;
+    st.episode_length[b] = ep_len;
+    st.episode_reward[b] = ep_rew;
+    st.score[b] = score;
+    st.possible[b] = possible;
+    const bool can = can_exit_now(st.min_performance[b], score, st.baseline[b], possible);
+    const uint16_t ev = (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
+    const int ne = min(st.exit_count[b], SL_MAX_EXITS);
+    for (int e = 0; e < ne; e++)
+        gb[st.exit_y[b * SL_MAX_EXITS + e] * W + st.exit_x[b * SL_MAX_EXITS + e]] = ev;
+    const bool times_up = ep_len > a.time_limit;
+    const bool over = st.game_over[b] != 0;
+    const bool completed = times_up || over;
+
+    double r = (double)r_int;
+    if (a.bonus_period > 0) {
+        const int n = a.bonus_period;
+        int len = st.prior_len[b], head = st.prior_head[b];
+        const int ax = st.agent_x[b], ay = st.agent_y[b];
+        int32_t *px = st.prior_x + b * SL_BONUS_PERIOD_MAX, *py = st.prior_y + b * SL_BONUS_PERIOD_MAX;
+        int dist;
+        if (len > 0) {
+            dist = abs(ax - px[head]) + abs(ay - py[head]) + (len < n ? n - len : 0);
+        } else {
+            dist = n;
+        }
+        dist = min(dist, a.bonus_len - 1);
+        r = r + a.bonus_table[dist];
+        if (len < n) {
+            const int slot = (head + len) % n;
+            px[slot] = ax;
+            py[slot] = ay;
+            st.prior_len[b] = len + 1;
+        } else {
+            px[head] = ax;
+            py[head] = ay;
+            st.prior_head[b] = (head + 1) % n;
+        }
+    }
+    r = r - (double)(side - st.side_effect[b]) * a.penalty_coef;
+    st.side_effect[b] = side;
+
+    reward_out[b] = r;
+    done_out[b] = (uint8_t)(a.auto_reset ? times_up : completed);
+    if (flags_out)
+        flags_out[b] = (uint8_t)((times_up ? 1 : 0) | (over ? 2 : 0) |
+                                 ((a.auto_reset && completed) ? 4 : 0));
+    if (ep_len_out) ep_len_out[b] = completed ? ep_len : 0;
+    if (ep_rew_out) ep_rew_out[b] = completed ? ep_rew : 0;
+}
+
+// ---------------------------------------------------------------------------
+// reset from the level pool
+// ---------------------------------------------------------------------------
+struct ResetArgs {
+    double wrapper_min_perf;
+    uint64_t seed;
+    uint32_t env0;
+    int32_t level_mode, n_total, augment;
+    int32_t bonus_period;
+};
+
+__global__ void __launch_bounds__(NT)
+k_env_reset(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ mask,
+            const uint8_t *__restrict__ flags, ResetArgs a) {
+    __shared__ int red[NT / 64][4];
+    __shared__ int wave_tot[NT / 64];
+    __shared__ int sh_exit_y[SL_MAX_EXITS], sh_exit_x[SL_MAX_EXITS];
+    __shared__ int sh_ev, sh_idx, sh_dy, sh_dx;
+    const int64_t b = blockIdx.x;
+    if (mask && !mask[b]) return;
+    if (flags && !(flags[b] & 4)) return;
+    const int H = st.H, W = st.W, hw = H * W;
+    const uint32_t gid = a.env0 + (uint32_t)b;
+    if (threadIdx.x == 0) {
+        const int ep = st.episodes[b];
+        int idx;
+        if (a.level_mode == 1) {
+            idx = (int)(philox_uniform(gid, (uint32_t)ep, 0x5EEDu, 2u, a.seed) * pool.K);
+        } else {
+            idx = (int)(((int64_t)gid + (int64_t)ep * a.n_total) % pool.K);
+        }
+        idx = min(max(idx, 0), pool.K - 1);
+        int dy = 0, dx = 0;
+        if (a.augment) {
+            dy = (int)(philox_uniform(gid, (uint32_t)ep, 0x0011u, 3u, a.seed) * H);
+            dx = (int)(philox_uniform(gid, (uint32_t)ep, 0x0022u, 3u, a.seed) * W);
+            dy = min(dy, H - 1);
+            dx = min(dx, W - 1);
+        }
+        sh_idx = idx; sh_dy = dy; sh_dx = dx;
+    }
+    __syncthreads();
+    const int idx = sh_idx, dy = sh_dy, dx = sh_dx;
+    const uint16_t *pb = pool.board + (int64_t)idx * hw, *pg = pool.goals + (int64_t)idx * hw;
+
+    // pass 1: reductions + ordered exit list of the (rolled) initial board
+    int acc[4] = {0, 0, 0, 0};   // points, score(=baseline), possible, exits
+    int n_exit = 0;
+    const int nchunk = (hw + NT - 1) / NT;
+    for (int c = 0; c < nchunk; c++) {
+        const int i = c * NT + threadIdx.x;
+        bool ex = false;
+        if (i < hw) {
+            const int y = i / W, x = i - y * W;
+            const int src = pymod(y - dy, H) * W + pymod(x - dx, W);
+            const uint32_t vb = pb[src], vg = pg[src];
+            int p, q, r;
+            cell_scores(vb, vg, &p, &q, &r);
+            acc[0] += p;
+            acc[1] += q;
+            acc[2] += r;
+            ex = (vb & EXIT) != 0;
+        }
+        int tot;
+        const int rank = block_rank(ex, wave_tot, &tot);
+        if (ex && n_exit + rank < SL_MAX_EXITS) {
+            sh_exit_y[n_exit + rank] = i / W;
+            sh_exit_x[n_exit + rank] = i % W;
+        }
+        n_exit += tot;
+    }
+    block_sum4(acc, red);
+    if (threadIdx.x == 0) {
+        const int points = acc[0], base = acc[1], possible = acc[2];
+        const double lvl_mp = pool.min_performance[idx];
+        const bool can = can_exit_now(lvl_mp, base, base, possible);
+        sh_ev = (int)(LEVEL_EXIT | (can ? COLOR_R : 0u));
+        const int ax = pymod(pool.agent_x[idx] + dx, W), ay = pymod(pool.agent_y[idx] + dy, H);
+        st.agent_x[b] = ax;
+        st.agent_y[b] = ay;
+        st.orientation[b] = pool.orientation[idx];
+        st.game_over[b] = 0;
+        st.num_steps[b] = 0;
+        st.episode_length[b] = 0;
+        st.episode_reward[b] = 0;
+        st.old_points[b] = points;
+        st.baseline[b] = base;
+        st.score[b] = base;
+        st.possible[b] = possible;
+        st.side_effect[b] = 0;
+        st.spawn_prob[b] = pool.spawn_prob[idx];
+        st.min_performance[b] = isnan(a.wrapper_min_perf) ? lvl_mp : a.wrapper_min_perf;
+        st.exit_count[b] = n_exit;
+        for (int e = 0; e < SL_MAX_EXITS; e++) {
+            st.exit_y[b * SL_MAX_EXITS + e] = (int16_t)(e < n_exit ? sh_exit_y[e] : 0);
+            st.exit_x[b * SL_MAX_EXITS + e] = (int16_t)(e < n_exit ? sh_exit_x[e] : 0);
+        }
+        st.prior_x[b * SL_BONUS_PERIOD_MAX] = ax;
+        st.prior_y[b * SL_BONUS_PERIOD_MAX] = ay;
+        st.prior_len[b] = 1;
+        st.prior_head[b] = 0;
+        st.level_index[b] = idx;
+        st.episodes[b] = st.episodes[b] + 1;
+    }
+    __syncthreads();
+    const uint16_t ev = (uint16_t)sh_ev;
+    uint16_t *gb = st.board + b * hw, *gg = st.goals + b * hw, *gs = st.start_board + b * hw;
+    for (int i = threadIdx.x; i < hw; i += NT) {
+        const int y = i / W, x = i - y * W;
+        const int src = pymod(y - dy, H) * W + pymod(x - dx, W);
+        const uint16_t vb = pb[src];
+        gs[i] = vb;
+        gb[i] = (vb & EXIT) ? ev : vb;
+        gg[i] = pg[src];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// observations
+// ---------------------------------------------------------------------------
+struct ObsArgs {
+    int vh, vw, remove_white, mode, nch;
+    int ch[16];
+};
+
+__device__ __forceinline__ uint16_t obs_value(uint32_t bv, uint32_t gv, int remove_white) {
+    uint32_t g = gv & COLORS;
+    if (remove_white && g == COLORS) g = 0;
+    return (uint16_t)((bv + (g << 3)) & 0xFFFFu);
+}
+
+__global__ void __launch_bounds__(NT)
+k_env_obs(sl_env_state st, ObsArgs a, void *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t view[];
+    const int64_t b = blockIdx.x;
+    const int H = st.H, W = st.W, hw = H * W, nv = a.vh * a.vw;
+    const uint16_t *gb = st.board + b * hw, *gg = st.goals + b * hw;
+    const int y0 = st.agent_y[b], x0 = st.agent_x[b];
+    const int ty = y0 - a.vh / 2, tx = x0 - a.vw / 2;
+    for (int i = threadIdx.x; i < nv; i += NT) {
+        const int r = i / a.vw, c = i - r * a.vw;
+        const int src = pymod(ty + r, H) * W + pymod(tx + c, W);
+        view[i] = obs_value(gb[src], gg[src], a.remove_white);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int ne = min(st.exit_count[b], SL_MAX_EXITS);
+        for (int e = 0; e < ne; e++) {
+            const int iy = st.exit_y[b * SL_MAX_EXITS + e], ix = st.exit_x[b * SL_MAX_EXITS + e];
+            int jy = pymod(iy - y0 + H / 2, H) - H / 2;
+            int jx = pymod(ix - x0 + W / 2, W) - W / 2;
+            jy = min(max(jy + a.vh / 2, 0), a.vh - 1);
+            jx = min(max(jx + a.vw / 2, 0), a.vw - 1);
+            view[jy * a.vw + jx] = obs_value(gb[iy * W + ix], gg[iy * W + ix], a.remove_white);
+        }
+    }
+    __syncthreads();
+    if (a.mode == SL_OBS_PACKED) {
+        uint16_t *o = (uint16_t *)out + b * nv;
+        for (int i = threadIdx.x; i < nv; i += NT) o[i] = view[i];
+    } else if (a.mode == SL_OBS_CHANNELS) {
+        uint16_t *o = (uint16_t *)out + b * (int64_t)nv * a.nch;
+        for (int j = threadIdx.x; j < nv * a.nch; j += NT) {
+            const int i = j / a.nch, k = j - i * a.nch;
+            o[j] = (uint16_t)((view[i] >> a.ch[k]) & 1u);
+        }
+    } else {
+        uint8_t *o = (uint8_t *)out + b * (int64_t)nv * a.nch;
+        for (int j = threadIdx.x; j < nv * a.nch; j += NT) {
+            const int i = j / a.nch, k = j - i * a.nch;
+            o[j] = (uint8_t)((view[i] >> a.ch[k]) & 1u);
+        }
+    }
+}
+
+bool set_lds(const void *fn, size_t bytes) {
+    if (bytes <= 65536) return true;
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) ==
+           hipSuccess;
+}
+
+bool state_ok(const sl_env_state *st) {
+    return st && st->B >= 0 && st->H >= 2 && st->W >= 2 && st->board && st->goals &&
+           st->start_board && (int64_t)st->H * st->W <= kMaxCells;
+}
+
+ResetArgs reset_args(const sl_env_cfg *cfg) {
+    ResetArgs r;
+    r.wrapper_min_perf = cfg->wrapper_min_performance;
+    r.seed = cfg->seed;
+    r.env0 = cfg->env0;
+    r.level_mode = cfg->level_mode;
+    r.n_total = cfg->n_total_envs > 0 ? cfg->n_total_envs : 1;
+    r.augment = cfg->augment_roll;
+    r.bonus_period = cfg->bonus_period;
+    return r;
+}
+
+}  // namespace
+
+extern "C" const char *sl_version(void) { return "safelife-hip 0.1 (gfx950)"; }
+
+extern "C" int sl_device_arch(char *buf, int len) {
+    int dev;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess)
+        return SL_EHIP;
+    int n = 0;
+    while (p.gcnArchName[n] && n < len - 1) {
+        buf[n] = p.gcnArchName[n];
+        n++;
+    }
+    if (len > 0) buf[n] = 0;
+    return SL_OK;
+}
+
+extern "C" int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const uint8_t *mask,
+                            const sl_env_cfg *cfg, void *stream) {
+    if (!state_ok(st) || !pool || !cfg || pool->K <= 0 || pool->H != st->H || pool->W != st->W)
+        return SL_EINVAL;
+    if (st->B == 0) return SL_OK;
+    hipLaunchKernelGGL(k_env_reset, dim3((unsigned)st->B), dim3(NT), 0, (hipStream_t)stream,
+                       *st, *pool, mask, (const uint8_t *)nullptr, reset_args(cfg));
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
+extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const int32_t *actions,
+                           const sl_env_cfg *cfg, double *reward, uint8_t *done,
+                           uint8_t *info_flags, int32_t *ep_len, int32_t *ep_reward,
+                           void *stream) {
+    if (!state_ok(st) || !cfg || !actions || !reward || !done || !cfg->scratch) return SL_EINVAL;
+    if (cfg->bonus_period < 0 || cfg->bonus_period > SL_BONUS_PERIOD_MAX) return SL_EINVAL;
+    if (cfg->bonus_period > 0 && (!cfg->bonus_table || cfg->bonus_len < 1)) return SL_EINVAL;
+    if (cfg->auto_reset && (!pool || !info_flags)) return SL_EINVAL;
+    const int64_t B = st->B;
+    if (B == 0) return SL_OK;
+    hipStream_t s = (hipStream_t)stream;
+    Scratch sc = scratch_of(cfg->scratch, B);
+    const size_t lds = (size_t)2 * st->H * st->W * sizeof(uint16_t);
+
+    hipLaunchKernelGGL(k_env_action, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, *st,
+                       actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act_reward);
+    if (hipGetLastError() != hipSuccess) return SL_EHIP;
+
+    StepArgs a;
+    a.time_limit = cfg->time_limit;
+    a.auto_reset = cfg->auto_reset;
+    a.bonus_len = cfg->bonus_len;
+    a.bonus_period = cfg->bonus_period;
+    a.penalty_coef = cfg->penalty_coef;
+    a.bonus_table = cfg->bonus_table;
+    a.seed = cfg->seed;
+    a.step = cfg->step;
+    a.env0 = cfg->env0;
+    a.draws = cfg->draws;
+    a.n_draws = cfg->n_draws;
+
+    if (cfg->rng_mode == SL_RNG_STREAM) {
+        if (!cfg->stream_pos || (!cfg->draws && cfg->n_draws > 0)) return SL_EINVAL;
+        if (!set_lds((const void *)k_env_count, lds)) return SL_ETOOBIG;
+        hipLaunchKernelGGL(k_env_count, dim3((unsigned)B), dim3(NT), lds, s, *st, sc.counts);
+        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        int rc = sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * B, cfg->stream_pos,
+                                       cfg->stream_pos, stream);
+        if (rc) return rc;
+        if (!set_lds((const void *)k_env_step_generic<SL_RNG_STREAM>, lds)) return SL_ETOOBIG;
+        hipLaunchKernelGGL(k_env_step_generic<SL_RNG_STREAM>, dim3((unsigned)B), dim3(NT), lds, s,
+                           *st, a, sc.act_reward, sc.offsets, sc.err, reward, done, info_flags,
+                           ep_len, ep_reward);
+    } else if (cfg->rng_mode == SL_RNG_PHILOX) {
+        if (!set_lds((const void *)k_env_step_generic<SL_RNG_PHILOX>, lds)) return SL_ETOOBIG;
+        hipLaunchKernelGGL(k_env_step_generic<SL_RNG_PHILOX>, dim3((unsigned)B), dim3(NT), lds, s,
+                           *st, a, sc.act_reward, sc.offsets, sc.err, reward, done, info_flags,
+                           ep_len, ep_reward);
+    } else {
+        return SL_EINVAL;
+    }
+    if (hipGetLastError() != hipSuccess) return SL_EHIP;
+
+    if (cfg->auto_reset) {
+        hipLaunchKernelGGL(k_env_reset, dim3((unsigned)B), dim3(NT), 0, s, *st, *pool,
+                           (const uint8_t *)nullptr, (const uint8_t *)info_flags,
+                           reset_args(cfg));
+        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+    }
+    return SL_OK;
+}
+
+extern "C" int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_white_goals,
+                          int obs_mode, const int32_t *channels, int nch, void *out,
+                          void *stream) {
+    if (!state_ok(st) || vh < 1 || vw < 1 || (int64_t)vh * vw > kMaxCells || !out)
+        return SL_EINVAL;
+    if (obs_mode != SL_OBS_PACKED && obs_mode != SL_OBS_CHANNELS && obs_mode != SL_OBS_CHANNELS_U8)
+        return SL_EINVAL;
+    ObsArgs a;
+    a.vh = vh;
+    a.vw = vw;
+    a.remove_white = remove_white_goals;
+    a.mode = obs_mode;
+    a.nch = 0;
+    if (obs_mode != SL_OBS_PACKED) {
+        if (!channels || nch < 1 || nch > 16) return SL_EINVAL;
+        a.nch = nch;
+        for (int k = 0; k < nch; k++) {
+            if (channels[k] < 0 || channels[k] > 15) return SL_EINVAL;
+            a.ch[k] = channels[k];
+        }
+    }
+    if (st->B == 0) return SL_OK;
+    const size_t lds = (size_t)vh * vw * sizeof(uint16_t);
+    if (!set_lds((const void *)k_env_obs, lds)) return SL_ETOOBIG;
+    hipLaunchKernelGGL(k_env_obs, dim3((unsigned)st->B), dim3(NT), lds, (hipStream_t)stream, *st,
+                       a, out);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
