@@ -58,6 +58,11 @@ extern "C" {
 const char *sl_version(void);
 int sl_device_arch(char *buf, int len);   /* e.g. "gfx950" */
 
+/* Timing events (hipEvent_t as void*) for in-process kernel timing. */
+int sl_event_create(void **ev);
+int sl_event_destroy(void *ev);
+int sl_event_elapsed_ms(void *begin, void *end, float *ms);   /* after completion */
+
 /* ---------------------------------------------------------------- boards -- */
 
 /*
@@ -150,6 +155,8 @@ typedef struct sl_env_cfg {
                                        1: Philox-random level                  */
     int32_t n_total_envs;           /* envs across all shards                  */
     int32_t augment_roll;           /* 1: random toroidal roll per episode     */
+    void *ev_begin, *ev_end;        /* optional hipEvent_t pair recorded around
+                                       the board-advance kernel (profiling)    */
 } sl_env_cfg;
 
 /*

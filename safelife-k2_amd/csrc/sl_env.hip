@@ -565,6 +565,24 @@ extern "C" int sl_device_arch(char *buf, int len) {
     return SL_OK;
 }
 
+extern "C" int sl_event_create(void **ev) {
+    if (!ev) return SL_EINVAL;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return SL_EHIP;
+    *ev = (void *)e;
+    return SL_OK;
+}
+
+extern "C" int sl_event_destroy(void *ev) {
+    return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? SL_OK : SL_EHIP;
+}
+
+extern "C" int sl_event_elapsed_ms(void *begin, void *end, float *ms) {
+    if (!begin || !end || !ms) return SL_EINVAL;
+    return hipEventElapsedTime(ms, (hipEvent_t)begin, (hipEvent_t)end) == hipSuccess ? SL_OK
+                                                                                    : SL_EHIP;
+}
+
 extern "C" int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const uint8_t *mask,
                             const sl_env_cfg *cfg, void *stream) {
     if (!state_ok(st) || !pool || !cfg || pool->K <= 0 || pool->H != st->H || pool->W != st->W)
@@ -620,6 +638,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
                            ep_len, ep_reward);
     } else if (cfg->rng_mode == SL_RNG_PHILOX) {
         if (!set_lds((const void *)k_env_step_generic<SL_RNG_PHILOX>, lds)) return SL_ETOOBIG;
+        if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
         hipLaunchKernelGGL(k_env_step_generic<SL_RNG_PHILOX>, dim3((unsigned)B), dim3(NT), lds, s,
                            *st, a, sc.act_reward, sc.offsets, sc.err, reward, done, info_flags,
                            ep_len, ep_reward);
@@ -627,6 +646,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         return SL_EINVAL;
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
+    if (cfg->ev_end) (void)hipEventRecord((hipEvent_t)cfg->ev_end, s);
 
     if (cfg->auto_reset) {
         hipLaunchKernelGGL(k_env_reset, dim3((unsigned)B), dim3(NT), 0, s, *st, *pool,

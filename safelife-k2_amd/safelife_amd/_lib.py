@@ -1,0 +1,127 @@
+"""ctypes binding of libsafelife_hip.so -- the C ABI declared in include/safelife_hip.h.
+
+The product path has no CPU fallback: if the HIP library is missing, or no GPU is
+visible, every entry point raises.
+"""
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_native", "libsafelife_hip.so")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+SL_OK, SL_EINVAL, SL_EHIP, SL_ETOOBIG = 0, -1, -2, -3
+SL_RNG_STREAM, SL_RNG_PHILOX = 0, 1
+SL_MAX_EXITS = 8
+SL_BONUS_PERIOD_MAX = 16
+SL_OBS_NONE, SL_OBS_PACKED, SL_OBS_CHANNELS, SL_OBS_CHANNELS_U8 = 0, 1, 2, 3
+
+_ERRORS = {SL_EINVAL: "invalid argument / shape", SL_EHIP: "HIP launch error",
+           SL_ETOOBIG: "board too large for this kernel"}
+
+vp = ctypes.c_void_p
+i32 = ctypes.c_int32
+i64 = ctypes.c_int64
+u32 = ctypes.c_uint32
+u64 = ctypes.c_uint64
+f32 = ctypes.c_float
+f64 = ctypes.c_double
+
+
+class EnvState(ctypes.Structure):
+    _fields_ = [("B", i64), ("H", i32), ("W", i32),
+                ("board", vp), ("goals", vp), ("start_board", vp),
+                ("agent_x", vp), ("agent_y", vp), ("orientation", vp),
+                ("game_over", vp), ("episode_length", vp), ("episode_reward", vp),
+                ("old_points", vp), ("baseline", vp), ("score", vp), ("possible", vp),
+                ("side_effect", vp), ("spawn_prob", vp), ("min_performance", vp),
+                ("prior_x", vp), ("prior_y", vp), ("prior_len", vp), ("prior_head", vp),
+                ("exit_count", vp), ("exit_y", vp), ("exit_x", vp),
+                ("level_index", vp), ("episodes", vp), ("num_steps", vp)]
+
+
+class LevelPool(ctypes.Structure):
+    _fields_ = [("K", i32), ("H", i32), ("W", i32),
+                ("board", vp), ("goals", vp), ("agent_x", vp), ("agent_y", vp),
+                ("orientation", vp), ("spawn_prob", vp), ("min_performance", vp)]
+
+
+class EnvCfg(ctypes.Structure):
+    _fields_ = [("time_limit", i32), ("auto_reset", i32),
+                ("can_toggle_powers", i32), ("can_toggle_colors", i32),
+                ("penalty_coef", f64), ("wrapper_min_performance", f64),
+                ("bonus_table", vp), ("bonus_len", i32), ("bonus_period", i32),
+                ("rng_mode", i32), ("seed", u64), ("step", u32), ("env0", u32),
+                ("draws", vp), ("n_draws", i64), ("stream_pos", vp), ("scratch", vp),
+                ("level_mode", i32), ("n_total_envs", i32), ("augment_roll", i32),
+                ("ev_begin", vp), ("ev_end", vp)]
+
+
+_lib = None
+
+
+class HipUnavailable(RuntimeError):
+    pass
+
+
+def build(force=False):
+    """Compile the HIP library in-tree (hipcc --offload-arch=gfx950)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", CSRC])
+
+
+def lib():
+    """Load the HIP library; raise if it is missing (there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HipUnavailable(
+            "libsafelife_hip.so not built (%s); run `make -C %s` -- the SafeLife HIP "
+            "path has no CPU fallback" % (LIB_PATH, CSRC))
+    L = ctypes.CDLL(LIB_PATH)
+    L.sl_version.restype = ctypes.c_char_p
+    L.sl_device_arch.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    L.sl_advance.argtypes = [vp, vp, i64, ctypes.c_int, ctypes.c_int, vp, f32, ctypes.c_int,
+                             u64, u32, u32, u32, vp, vp, vp]
+    L.sl_count_eligible.argtypes = [vp, vp, i64, ctypes.c_int, ctypes.c_int, vp]
+    L.sl_exclusive_scan_i64.argtypes = [vp, vp, i64, vp, vp, vp]
+    L.sl_env_step.argtypes = [ctypes.POINTER(EnvState), ctypes.POINTER(LevelPool), vp,
+                              ctypes.POINTER(EnvCfg), vp, vp, vp, vp, vp, vp]
+    L.sl_env_reset.argtypes = [ctypes.POINTER(EnvState), ctypes.POINTER(LevelPool), vp,
+                               ctypes.POINTER(EnvCfg), vp]
+    L.sl_env_obs.argtypes = [ctypes.POINTER(EnvState), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                             ctypes.c_int, vp, ctypes.c_int, vp, vp]
+    L.sl_event_create.argtypes = [ctypes.POINTER(vp)]
+    L.sl_event_destroy.argtypes = [vp]
+    L.sl_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(f32)]
+    for name in ("sl_event_create", "sl_event_destroy", "sl_event_elapsed_ms", "sl_device_arch", "sl_advance", "sl_count_eligible", "sl_exclusive_scan_i64",
+                 "sl_env_step", "sl_env_reset", "sl_env_obs"):
+        getattr(L, name).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != SL_OK:
+        raise RuntimeError("%s failed: %s (code %d)" % (what, _ERRORS.get(rc, "?"), rc))
+
+
+def require_device(device=None):
+    """The torch device to run on; raises when no GPU is visible."""
+    import torch
+    if not torch.cuda.is_available():
+        raise HipUnavailable("no ROCm GPU visible: the SafeLife HIP path needs an MI355X "
+                             "(gfx950); there is no CPU fallback")
+    lib()
+    return torch.device(device if device is not None else "cuda:%d" % torch.cuda.current_device())
+
+
+def stream_ptr(device):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None

@@ -1,0 +1,141 @@
+"""Drop-in for the reference's C extension ``safelife.speedups`` (hot entries only).
+
+    advance_board(board, spawn_prob=0.3) -> new uint16 board      module.c:19-44
+    seed(i)                                                       module.c:246-253
+
+Both run on the GPU through libsafelife_hip.so.  Spawn draws follow the reference
+exactly: a 10 000-double buffer refilled from the *global* numpy RNG
+(``np.random.random(10000)``, random.c:14-26), one draw per eligible cell in
+row-major order (random.c:47-52), compared as ``u < (double)(float)spawn_prob``.
+The number of draws a board needs is counted on the GPU first, the host takes that
+many doubles from the emulated buffer, and the board is advanced on the GPU.
+
+Deliberate divergences: a non-2-d or empty board raises ValueError (the reference
+returns NULL without an exception, i.e. SystemError); H or W == 1 raises ValueError
+(undefined behaviour in the reference).
+
+``advance_boards`` is the batched device entry (torch uint16 [B,H,W] in and out).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+_RAND_BUFFER_SIZE = 10000
+
+
+class _RefBuffer:
+    def __init__(self):
+        self.buf = None
+        self.pos = _RAND_BUFFER_SIZE
+
+    def refill(self):
+        self.buf = np.random.random(_RAND_BUFFER_SIZE)
+        self.pos = 0
+
+    def take(self, n):
+        parts = []
+        while n > 0:
+            if self.pos >= _RAND_BUFFER_SIZE:
+                self.refill()
+            k = min(n, _RAND_BUFFER_SIZE - self.pos)
+            parts.append(self.buf[self.pos:self.pos + k])
+            self.pos += k
+            n -= k
+        return np.concatenate(parts) if parts else np.zeros(0)
+
+
+_buffer = _RefBuffer()
+
+
+def seed(i):
+    """np.random.seed(i) followed by an immediate buffer refill (random.c:28-45)."""
+    i = int(i)
+    if not 0 <= i <= 0xFFFFFFFF:
+        raise OverflowError("seed must be an unsigned 32-bit int")
+    np.random.seed(i)
+    _buffer.refill()
+
+
+def _to_device_board(board, device):
+    import torch
+    if isinstance(board, torch.Tensor):
+        t = board
+        if t.dtype != torch.uint16:
+            t = t.to(torch.int64).remainder(65536).to(torch.int32).to(torch.uint16)
+        return t.to(device).contiguous(), True
+    a = np.asarray(board)
+    if a.dtype != np.uint16:
+        a = a.astype(np.uint16)           # NPY_ARRAY_FORCECAST
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device), False
+
+
+def advance_board(board, spawn_prob=0.3):
+    """Advance one board; returns a new array (numpy in -> numpy out, torch -> torch)."""
+    import torch
+    device = _lib.require_device()
+    t, is_torch = _to_device_board(board, device)
+    if t.dim() != 2 or t.numel() == 0:
+        raise ValueError("advance_board expects a non-empty 2-d board")
+    H, W = t.shape
+    if H < 2 or W < 2:
+        raise ValueError("advance_board needs H, W >= 2")
+    p = float(np.float32(spawn_prob))
+    L = _lib.lib()
+    s = _lib.stream_ptr(device)
+    cnt = torch.zeros(1, dtype=torch.int64, device=device)
+    _lib.check(L.sl_count_eligible(t.data_ptr(), cnt.data_ptr(), 1, H, W, s), "sl_count_eligible")
+    n = int(cnt.item())
+    draws = _buffer.take(n)               # consumed whatever p is, as random_float() is
+    d = torch.from_numpy(draws if n else np.zeros(1)).to(device)
+    off = torch.zeros(1, dtype=torch.int64, device=device)
+    out = torch.empty_like(t)
+    _lib.check(L.sl_advance(t.data_ptr(), out.data_ptr(), 1, H, W, None, p, _lib.SL_RNG_STREAM,
+                            0, 0, 0, 0, d.data_ptr(), off.data_ptr(), s), "sl_advance")
+    if is_torch:
+        return out
+    return out.cpu().numpy()
+
+
+def advance_boards(boards, spawn_prob=0.3, rng="philox", seed=0, env0=0, step=0, tensor=0,
+                   draws=None, draw_offsets=None, out=None):
+    """Batched device advance: boards uint16 [B,H,W] (torch, on the GPU).
+
+    rng="philox": spawn uniforms from Philox(seed; cell, env0+b, step, tensor).
+    rng="stream": board b takes draws[draw_offsets[b] + k] for its k-th eligible cell.
+    spawn_prob: a float or a float32 tensor [B].
+    """
+    import torch
+    device = _lib.require_device()
+    if boards.dim() != 3 or boards.dtype != torch.uint16:
+        raise ValueError("boards must be a uint16 [B,H,W] tensor")
+    boards = boards.to(device).contiguous()
+    B, H, W = boards.shape
+    if out is None:
+        out = torch.empty_like(boards)
+    sp_ptr, sp_scalar = None, 0.3
+    if isinstance(spawn_prob, torch.Tensor):
+        sp = spawn_prob.to(device=device, dtype=torch.float32).contiguous()
+        sp_ptr = sp.data_ptr()
+    else:
+        sp_scalar = float(np.float32(spawn_prob))
+    mode = _lib.SL_RNG_PHILOX if rng == "philox" else _lib.SL_RNG_STREAM
+    dp = draws.data_ptr() if draws is not None else None
+    op = draw_offsets.data_ptr() if draw_offsets is not None else None
+    _lib.check(_lib.lib().sl_advance(boards.data_ptr(), out.data_ptr(), B, H, W, sp_ptr,
+                                     sp_scalar, mode, seed & 0xFFFFFFFFFFFFFFFF, env0, step,
+                                     tensor, dp, op, _lib.stream_ptr(device)), "sl_advance")
+    return out
+
+
+def count_eligible(boards):
+    """Draws each board of a uint16 [B,H,W] device tensor consumes in one advance."""
+    import torch
+    device = _lib.require_device()
+    boards = boards.to(device).contiguous()
+    B, H, W = boards.shape
+    cnt = torch.zeros(B, dtype=torch.int64, device=device)
+    _lib.check(_lib.lib().sl_count_eligible(boards.data_ptr(), cnt.data_ptr(), B, H, W,
+                                            _lib.stream_ptr(device)), "sl_count_eligible")
+    return cnt

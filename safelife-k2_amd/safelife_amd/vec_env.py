@@ -1,0 +1,290 @@
+"""SafeLifeVecEnv: B SafeLife episodes stepped together on one MI355X.
+
+Semantics are those of the reference's PPO training chain, stepped env by env:
+
+    env = SafeLifeEnv(level_iterator, view_shape=...)          safelife_env.py:87-198
+    env = MovementBonusWrapper(env)                            env_wrappers.py:39-94
+    env = SimpleSideEffectPenalty(env, penalty_coef=..., min_performance=...)
+                                                               env_wrappers.py:306-346
+    env = ContinuingEnv(env)                                   env_wrappers.py:289-303
+    ... and PPO.run_agents resets an env whenever done         training/ppo.py:441-445
+(wiring: training/safelife_ppo.py:128-139; the logging-only RecordingSafeLifeWrapper
+is not part of the stepped path).
+
+Everything per step runs in HIP kernels through the C ABI (include/safelife_hip.h);
+the host only fills scalar arguments.  There is no CPU fallback.
+
+RNG: ``rng="philox"`` (default) draws each spawn uniform from Philox4x32-10 keyed by
+(seed; cell, global env id, step, tensor), so results do not depend on how the
+batch is sharded.  ``rng="stream"`` replays a supplied uniform stream in the
+reference's order (env by env, board then goals, row-major eligible cells), which
+is how the reference's global-numpy buffer (speedups_src/random.c) is matched.
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _lib
+from .levels import LevelPool
+
+ACTION_NAMES = ("NULL", "MOVE UP", "MOVE RIGHT", "MOVE DOWN", "MOVE LEFT",
+                "TOGGLE UP", "TOGGLE RIGHT", "TOGGLE DOWN", "TOGGLE LEFT")
+
+
+class GlobalCounter:
+    """Host mirror of SafeLifeEnv.global_counter (safelife_env.py:81-85)."""
+
+    def __init__(self):
+        self.episodes_started = 0
+        self.episodes_completed = 0
+        self.num_steps = 0
+
+
+def _sched(val, counter):
+    # BaseWrapper.scheduled (env_wrappers.py:29-36)
+    return val(counter.num_steps) if callable(val) else val
+
+
+class SafeLifeVecEnv:
+    action_names = ACTION_NAMES
+
+    def __init__(self, levels, num_envs, device=None, *, time_limit=1000,
+                 view_shape=(15, 15), output_channels=tuple(range(15)),
+                 remove_white_goals=True, movement_bonus=0.1, movement_bonus_power=0.01,
+                 movement_bonus_period=4, penalty_coef=0.0, min_performance=0.01,
+                 auto_reset=True, rng="philox", seed=0, spawn_stream=None,
+                 level_order="sequential", augment_roll=False, env0=0, n_total_envs=None,
+                 can_toggle_powers=False, can_toggle_colors=False, obs_dtype="uint16",
+                 compute_obs=True, global_counter=None):
+        import torch
+        self.torch = torch
+        self.device = _lib.require_device(device)
+        self.pool = levels if isinstance(levels, LevelPool) else LevelPool.from_levels(levels)
+        self.B = int(num_envs)
+        self.H, self.W = self.pool.H, self.pool.W
+        self.time_limit = int(time_limit)
+        self.view_shape = tuple(int(v) for v in view_shape)
+        self.output_channels = tuple(output_channels) if output_channels else None
+        self.remove_white_goals = bool(remove_white_goals)
+        self.movement_bonus = movement_bonus
+        self.movement_bonus_power = movement_bonus_power
+        self.movement_bonus_period = int(movement_bonus_period)
+        if not 0 <= self.movement_bonus_period <= _lib.SL_BONUS_PERIOD_MAX:
+            raise ValueError("movement_bonus_period must be in [0, %d]" % _lib.SL_BONUS_PERIOD_MAX)
+        self.penalty_coef = penalty_coef
+        self.min_performance = min_performance
+        self.auto_reset = bool(auto_reset)
+        self.rng = rng
+        self.seed = int(seed)
+        self.level_order = level_order
+        self.augment_roll = bool(augment_roll)
+        self.env0 = int(env0)
+        self.n_total_envs = int(n_total_envs) if n_total_envs else self.B
+        self.can_toggle_powers = bool(can_toggle_powers)
+        self.can_toggle_colors = bool(can_toggle_colors)
+        self.compute_obs = bool(compute_obs)
+        self.global_counter = global_counter if global_counter is not None else GlobalCounter()
+        self._step_index = 0
+        self._alloc(obs_dtype)
+        if rng == "stream":
+            if spawn_stream is None:
+                raise ValueError("rng='stream' needs spawn_stream (uniform doubles)")
+            self.set_spawn_stream(spawn_stream)
+        elif rng != "philox":
+            raise ValueError("rng must be 'philox' or 'stream'")
+        self._bonus_key = None
+
+    # ------------------------------------------------------------------ setup
+    def _alloc(self, obs_dtype):
+        torch, dev, B, H, W = self.torch, self.device, self.B, self.H, self.W
+        z = lambda *s, dt=torch.int32: torch.zeros(s, dtype=dt, device=dev)
+        self.board = z(B, H, W, dt=torch.uint16)
+        self.goals = z(B, H, W, dt=torch.uint16)
+        self.start_board = z(B, H, W, dt=torch.uint16)
+        self.st_t = {
+            "agent_x": z(B), "agent_y": z(B), "orientation": z(B), "game_over": z(B),
+            "episode_length": z(B), "episode_reward": z(B), "old_points": z(B),
+            "baseline": z(B), "score": z(B), "possible": z(B), "side_effect": z(B),
+            "spawn_prob": z(B, dt=torch.float32), "min_performance": z(B, dt=torch.float64),
+            "prior_x": z(B, _lib.SL_BONUS_PERIOD_MAX), "prior_y": z(B, _lib.SL_BONUS_PERIOD_MAX),
+            "prior_len": z(B), "prior_head": z(B), "exit_count": z(B),
+            "exit_y": z(B, _lib.SL_MAX_EXITS, dt=torch.int16),
+            "exit_x": z(B, _lib.SL_MAX_EXITS, dt=torch.int16),
+            "level_index": z(B), "episodes": z(B), "num_steps": z(B),
+        }
+        s = _lib.EnvState()
+        s.B, s.H, s.W = B, H, W
+        s.board, s.goals, s.start_board = (self.board.data_ptr(), self.goals.data_ptr(),
+                                           self.start_board.data_ptr())
+        for k, t in self.st_t.items():
+            setattr(s, k, t.data_ptr())
+        self._state = s
+        self.actions_dev = z(B)
+        self.reward = z(B, dt=torch.float64)
+        self.done = z(B, dt=torch.uint8)
+        self.flags = z(B, dt=torch.uint8)
+        self.ep_len = z(B)
+        self.ep_rew = z(B)
+        self.scratch = z(5 * B + 16, dt=torch.int64)
+        self.stream_pos = z(1, dt=torch.int64)
+        vh, vw = self.view_shape
+        if self.output_channels is None:
+            self.obs_mode = _lib.SL_OBS_PACKED
+            self.obs = z(B, vh, vw, dt=torch.uint16)
+        else:
+            nch = len(self.output_channels)
+            if obs_dtype == "uint8":
+                self.obs_mode = _lib.SL_OBS_CHANNELS_U8
+                self.obs = z(B, vh, vw, nch, dt=torch.uint8)
+            else:
+                self.obs_mode = _lib.SL_OBS_CHANNELS
+                self.obs = z(B, vh, vw, nch, dt=torch.uint16)
+            self._channels = (ctypes.c_int32 * nch)(*self.output_channels)
+        self._pool_dev = self.pool.to_device(self.device)
+        self._cfg = _lib.EnvCfg()
+
+    def set_spawn_stream(self, stream, pos=0):
+        """Uniform doubles consumed in reference order (rng='stream')."""
+        torch = self.torch
+        s = torch.as_tensor(np.ascontiguousarray(stream, dtype=np.float64)).to(self.device)
+        self.spawn_stream = s
+        self.stream_pos.fill_(int(pos))
+
+    def _bonus_table(self):
+        key = (self.movement_bonus, self.movement_bonus_power, self.movement_bonus_period)
+        if self._bonus_key != key:
+            n = self.movement_bonus_period
+            dmax = self.H + self.W + n + 2
+            # evaluated in Python exactly as MovementBonusWrapper.step does
+            vals = [self.movement_bonus * (d / n) ** self.movement_bonus_power if n else 0.0
+                    for d in range(dmax)]
+            self._bonus_t = self.torch.tensor(vals, dtype=self.torch.float64, device=self.device)
+            self._bonus_key = key
+        return self._bonus_t
+
+    def _fill_cfg(self):
+        c = self._cfg
+        gc = self.global_counter
+        c.time_limit = self.time_limit
+        c.auto_reset = int(self.auto_reset)
+        c.can_toggle_powers = int(self.can_toggle_powers)
+        c.can_toggle_colors = int(self.can_toggle_colors)
+        c.penalty_coef = float(_sched(self.penalty_coef, gc))
+        mp = _sched(self.min_performance, gc)
+        c.wrapper_min_performance = float("nan") if mp is None else float(mp)
+        bt = self._bonus_table()
+        c.bonus_table = bt.data_ptr()
+        c.bonus_len = bt.numel()
+        c.bonus_period = self.movement_bonus_period
+        c.rng_mode = _lib.SL_RNG_STREAM if self.rng == "stream" else _lib.SL_RNG_PHILOX
+        c.seed = self.seed & 0xFFFFFFFFFFFFFFFF
+        c.step = self._step_index & 0xFFFFFFFF
+        c.env0 = self.env0
+        if self.rng == "stream":
+            c.draws = self.spawn_stream.data_ptr()
+            c.n_draws = self.spawn_stream.numel()
+        else:
+            c.draws = None
+            c.n_draws = 0
+        c.stream_pos = self.stream_pos.data_ptr()
+        c.scratch = self.scratch.data_ptr()
+        c.level_mode = 1 if self.level_order == "random" else 0
+        c.n_total_envs = self.n_total_envs
+        c.augment_roll = int(self.augment_roll)
+        return c
+
+    # -------------------------------------------------------------- gym-ish API
+    def reset(self, mask=None):
+        """Reset all envs (or those with mask[b] != 0); returns observations."""
+        L = _lib.lib()
+        cfg = self._fill_cfg()
+        m = None
+        if mask is not None:
+            m = self.torch.as_tensor(mask, device=self.device).to(self.torch.uint8).contiguous()
+        _lib.check(L.sl_env_reset(ctypes.byref(self._state), ctypes.byref(self._pool_dev["struct"]),
+                                  _lib.ptr(m), ctypes.byref(cfg), _lib.stream_ptr(self.device)),
+                   "sl_env_reset")
+        self.global_counter.episodes_started += self.B if mask is None else int(
+            self.torch.count_nonzero(m).item())
+        return self.observe() if self.compute_obs else None
+
+    def observe(self):
+        L = _lib.lib()
+        vh, vw = self.view_shape
+        ch = self._channels if self.obs_mode != _lib.SL_OBS_PACKED else None
+        nch = len(self.output_channels) if self.output_channels else 0
+        _lib.check(L.sl_env_obs(ctypes.byref(self._state), vh, vw, int(self.remove_white_goals),
+                                self.obs_mode, ch, nch, self.obs.data_ptr(),
+                                _lib.stream_ptr(self.device)), "sl_env_obs")
+        return self.obs
+
+    def step(self, actions):
+        """One env-step for every env.  `actions`: int [B] (torch or numpy), 0..8.
+
+        Returns (obs, reward float64 [B], done bool [B], info) as device tensors.
+        Envs that finished are already reset (ContinuingEnv + run_agents semantics);
+        their obs are those of the new episode.
+        """
+        self.step_async(actions)
+        return self.step_wait()
+
+    def step_async(self, actions):
+        torch = self.torch
+        a = torch.as_tensor(actions)
+        if a.device != self.device or a.dtype != torch.int32:
+            a = a.to(device=self.device, dtype=torch.int32)
+        self.actions_dev.copy_(a.reshape(self.B))
+        L = _lib.lib()
+        cfg = self._fill_cfg()
+        _lib.check(L.sl_env_step(ctypes.byref(self._state), ctypes.byref(self._pool_dev["struct"]),
+                                 self.actions_dev.data_ptr(), ctypes.byref(cfg),
+                                 self.reward.data_ptr(), self.done.data_ptr(),
+                                 self.flags.data_ptr(), self.ep_len.data_ptr(),
+                                 self.ep_rew.data_ptr(), _lib.stream_ptr(self.device)),
+                   "sl_env_step")
+        self._step_index += 1
+        self.global_counter.num_steps += self.B
+        if self.compute_obs:
+            self.observe()
+
+    def step_wait(self):
+        info = {"times_up": (self.flags & 1) != 0, "game_over": (self.flags & 2) != 0,
+                "reset": (self.flags & 4) != 0, "episode_length": self.ep_len,
+                "episode_reward": self.ep_rew}
+        return (self.obs if self.compute_obs else None), self.reward, self.done.bool(), info
+
+    # ---------------------------------------------------------------- helpers
+    @property
+    def state(self):
+        """Per-env scalar state tensors (agent_x, agent_y, orientation, ...)."""
+        return self.st_t
+
+    def stream_error(self):
+        """True if rng='stream' ran past the end of the supplied stream."""
+        return bool(self.scratch[5 * self.B].item() & 1)
+
+    def set_state(self, board, goals, start_board, **scalars):
+        """Load explicit state (for tests / checkpoints).  Arrays are [B,...]."""
+        torch = self.torch
+        for dst, src in ((self.board, board), (self.goals, goals), (self.start_board, start_board)):
+            dst.copy_(torch.as_tensor(np.ascontiguousarray(src, dtype=np.uint16)).to(self.device))
+        for k, v in scalars.items():
+            t = self.st_t[k]
+            t.copy_(torch.as_tensor(np.asarray(v)).to(device=self.device, dtype=t.dtype))
+
+    def state_dict(self):
+        d = {"board": self.board.clone(), "goals": self.goals.clone(),
+             "start_board": self.start_board.clone(), "step_index": self._step_index,
+             "stream_pos": self.stream_pos.clone()}
+        d.update({k: v.clone() for k, v in self.st_t.items()})
+        return d
+
+    def load_state_dict(self, d):
+        self.board.copy_(d["board"])
+        self.goals.copy_(d["goals"])
+        self.start_board.copy_(d["start_board"])
+        for k, v in self.st_t.items():
+            v.copy_(d[k])
+        self._step_index = int(d["step_index"])
+        self.stream_pos.copy_(d["stream_pos"])

@@ -1,0 +1,265 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and the golden vectors.
+
+All tests here need the MI355X.  Integer/board results must be bit-exact; rewards
+are float64 and are required to be bit-exact too (the kernel evaluates the same
+IEEE operations in the same order; the tolerance the north star allows is 1e-6).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+pytestmark = pytest.mark.gpu
+REWARD_TOL = 1e-6   # north_star bound; the checks below are stricter (==)
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    import safelife_amd  # noqa: F401
+    return torch, torch.device("cuda:0")
+
+
+# --------------------------------------------------------------------- board
+def test_advance_known_answers(torch_dev):
+    torch, dev = torch_dev
+    from safelife_amd import speedups
+    d = np.load(os.path.join(GOLDEN, "advance_known_answers.npz"))
+    groups = {}
+    off = 0
+    for (H, W), p in zip(d["shapes"], d["spawn_prob"]):
+        n = H * W
+        groups.setdefault((int(H), int(W), float(p)), []).append(
+            (d["boards_in"][off:off + n].reshape(H, W), d["boards_out"][off:off + n].reshape(H, W)))
+        off += n
+    for (H, W, p), items in groups.items():
+        bi = torch.from_numpy(np.stack([x[0] for x in items])).to(dev)
+        out = speedups.advance_boards(bi, p, rng="stream")
+        assert np.array_equal(out.cpu().numpy(), np.stack([x[1] for x in items])), (H, W, p)
+
+
+def test_speedups_dropin_reference_stream(torch_dev):
+    from safelife_amd import speedups
+    d = np.load(os.path.join(GOLDEN, "advance_stream.npz"))
+    keys = sorted({k.rsplit("_", 1)[0] for k in d.files if k.endswith("_board0")})
+    for key in keys:
+        s = int(key.split("_")[0][1:])
+        speedups.seed(s)
+        b, g = d[key + "_board0"], d[key + "_goals0"]
+        for t in range(d[key + "_boards"].shape[0]):
+            b = speedups.advance_board(b, 0.3)
+            g = speedups.advance_board(g, 0.3)
+            assert b.dtype == np.uint16
+            assert np.array_equal(b, d[key + "_boards"][t]), (key, t)
+            assert np.array_equal(g, d[key + "_goals"][t]), (key, t)
+
+
+def _random_boards(rng, B, H, W, spawners=True):
+    b = np.where(rng.rand(B, H, W) < 0.3, 9, 0).astype(np.uint16)
+    b |= (rng.randint(0, 8, size=(B, H, W)) << 9).astype(np.uint16) * (b > 0)
+    if spawners:
+        b[rng.rand(B, H, W) < 0.03] = 152
+        b[rng.rand(B, H, W) < 0.01] = 144 | (2 << 9)
+    b[rng.rand(B, H, W) < 0.01] = 64
+    b[rng.rand(B, H, W) < 0.01] = 32 | 16
+    b[rng.rand(B, H, W) < 0.01] = 0x8000 | 4 | 16
+    return b
+
+
+@pytest.mark.parametrize("shape", [(2, 2), (3, 5), (25, 25), (26, 26), (64, 64), (17, 128),
+                                   (128, 128)])
+def test_advance_philox_vs_oracle(torch_dev, shape):
+    torch, dev = torch_dev
+    from safelife_amd import speedups
+    H, W = shape
+    rng = np.random.RandomState(H * 1000 + W)
+    B = 24
+    b = _random_boards(rng, B, H, W)
+    p = np.float32(0.3)
+    out = speedups.advance_boards(torch.from_numpy(b).to(dev), float(p), rng="philox", seed=77,
+                                  env0=5, step=9, tensor=1).cpu().numpy()
+    for i in range(B):
+        ref, _ = oracle.advance(b[i], p, rng=oracle.RNG_PHILOX, seed=77, env_id=5 + i, step=9,
+                                tensor=1)
+        assert np.array_equal(out[i], ref), i
+
+
+def test_advance_stream_batched_vs_oracle(torch_dev):
+    torch, dev = torch_dev
+    from safelife_amd import speedups
+    rng = np.random.RandomState(4)
+    B, H, W = 40, 26, 26
+    b = _random_boards(rng, B, H, W)
+    tb = torch.from_numpy(b).to(dev)
+    counts = speedups.count_eligible(tb).cpu().numpy()
+    offs = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    stream = rng.random_sample(int(counts.sum()) + 1)
+    out = speedups.advance_boards(tb, 0.3, rng="stream", draws=torch.from_numpy(stream).to(dev),
+                                  draw_offsets=torch.from_numpy(offs).to(dev)).cpu().numpy()
+    for i in range(B):
+        assert oracle.count_eligible(b[i]) == counts[i]
+        ref, pos = oracle.advance(b[i], 0.3, stream, offs[i])
+        assert pos == offs[i] + counts[i]
+        assert np.array_equal(out[i], ref), i
+
+
+# ----------------------------------------------------------------------- env
+def _traj_files():
+    return sorted(glob.glob(os.path.join(GOLDEN, "traj_*.npz")))
+
+
+def _vec_env_from_traj(d, B=1, **kw):
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    penalty, min_perf, seed, vh, vw, time_limit = d["cfg"]
+    pool = LevelPool.from_levels([{
+        "board": d["level_board"], "goals": d["level_goals"], "agent_loc": d["level_agent_loc"],
+        "orientation": d["level_orientation"], "spawn_prob": d["level_spawn_prob"],
+        "min_performance": d["level_min_performance"]}])
+    stream = np.random.RandomState(int(seed)).random_sample(400000)
+    args = dict(time_limit=int(time_limit), view_shape=(int(vh), int(vw)), output_channels=None,
+                penalty_coef=float(penalty), min_performance=float(min_perf), rng="stream",
+                spawn_stream=stream)
+    args.update(kw)
+    return SafeLifeVecEnv(pool, B, "cuda:0", **args)
+
+
+@pytest.mark.parametrize("path", _traj_files(), ids=lambda p: os.path.basename(p)[5:-4])
+def test_env_golden_trajectory(torch_dev, path):
+    torch, dev = torch_dev
+    d = np.load(path)
+    env = _vec_env_from_traj(d)
+    obs = env.reset().cpu().numpy()
+    assert np.array_equal(obs[0], d["obs0"])
+    T = len(d["action"])
+    actions = torch.from_numpy(d["action"].astype(np.int32)).to(dev)
+    for t in range(T):
+        obs, r, done, info = env.step(actions[t:t + 1])
+        ctx = (os.path.basename(path), t)
+        assert r.item() == d["reward"][t], (ctx, r.item(), d["reward"][t])
+        assert bool(done.item()) == bool(d["done"][t]), ctx
+        assert bool(info["times_up"].item()) == bool(d["times_up"][t]), ctx
+        if not (d["done"][t] or d["game_over"][t]):
+            st = env.state
+            assert (st["agent_x"].item(), st["agent_y"].item()) == tuple(d["agent_loc"][t]), ctx
+            assert st["orientation"].item() == d["orientation"][t], ctx
+            assert st["old_points"].item() == d["points"][t], ctx
+            assert st["side_effect"].item() == d["side_effect"][t], ctx
+        assert np.array_equal(env.board[0].cpu().numpy(), d["board"][t]), ctx
+        assert np.array_equal(env.goals[0].cpu().numpy(), d["goals"][t]), ctx
+        assert np.array_equal(obs[0].cpu().numpy(), d["obs"][t]), ctx
+    assert not env.stream_error()
+
+
+def _oracle_envs(pool_levels, B, **kw):
+    envs = []
+    for e in range(B):
+        envs.append(oracle.OracleEnv(lambda ep, e=e: pool_levels[(e + ep * B) % len(pool_levels)],
+                                     env_id=e, **kw))
+    return envs
+
+
+def _levels_from_pool(path):
+    d = np.load(path)
+    return [oracle.Level(d["board"][k], d["goals"][k], d["agent_loc"][k], d["orientation"][k],
+                         d["spawn_prob"][k], d["min_performance"][k])
+            for k in range(d["board"].shape[0])]
+
+
+@pytest.mark.parametrize("pool_name,rng_mode", [("c2_append_still_25", "philox"),
+                                                ("c3_prune_still_64", "philox"),
+                                                ("c2_append_still_25", "stream")])
+def test_env_batch_vs_oracle(torch_dev, pool_name, rng_mode):
+    """B envs with mixed levels, random actions, short time limit (exercises resets)."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    path = os.path.join(GOLDEN, "pools", pool_name + ".npz")
+    levels = _levels_from_pool(path)
+    B, T = 24, 90
+    kw = dict(time_limit=40, view_shape=(15, 15), output_channels=None, penalty_coef=0.7,
+              min_performance=-1.0)
+    rng = np.random.RandomState(7)
+    stream = rng.random_sample(300000)
+    if rng_mode == "stream":
+        venv = SafeLifeVecEnv(LevelPool.load(path), B, "cuda:0", rng="stream",
+                              spawn_stream=stream, **kw)
+        shared = _SharedStream(stream)
+        oenvs = _oracle_envs(levels, B, rng="stream", stream=shared, **kw)
+    else:
+        venv = SafeLifeVecEnv(LevelPool.load(path), B, "cuda:0", rng="philox", seed=123, **kw)
+        oenvs = _oracle_envs(levels, B, rng="philox", seed=123, **kw)
+    vo = venv.reset().cpu().numpy()
+    for e in range(B):
+        assert np.array_equal(vo[e], oenvs[e].reset()), e
+    for t in range(T):
+        acts = rng.randint(0, 9, size=B).astype(np.int32)
+        vo, vr, vd, info = venv.step(torch.from_numpy(acts).to(dev))
+        vo, vr, vd = vo.cpu().numpy(), vr.cpu().numpy(), vd.cpu().numpy()
+        vb, vg = venv.board.cpu().numpy(), venv.goals.cpu().numpy()
+        for e in range(B):
+            o, r, dn, _ = oenvs[e].step(int(acts[e]))
+            ctx = (t, e)
+            assert vr[e] == r, (ctx, vr[e], r)
+            assert bool(vd[e]) == dn, ctx
+            assert np.array_equal(vb[e], oenvs[e].board), ctx
+            assert np.array_equal(vg[e], oenvs[e].goals), ctx
+            assert np.array_equal(vo[e], o), ctx
+
+
+class _SharedStream:
+    """One uniform stream consumed env after env, board then goals (replay order)."""
+
+    def __init__(self, s):
+        self.s, self.pos = s, 0
+
+    def take(self, n):
+        out = self.s[self.pos:self.pos + n]
+        self.pos += n
+        return out
+
+
+def test_obs_channels_vs_packed(torch_dev):
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    pool = LevelPool.load(os.path.join(GOLDEN, "pools", "c2_append_still_25.npz"))
+    kw = dict(view_shape=(33, 33), rng="philox", seed=3)
+    e1 = SafeLifeVecEnv(pool, 16, "cuda:0", output_channels=None, **kw)
+    e2 = SafeLifeVecEnv(pool, 16, "cuda:0", output_channels=tuple(range(15)), **kw)
+    e3 = SafeLifeVecEnv(pool, 16, "cuda:0", output_channels=(0, 9, 12, 15), obs_dtype="uint8",
+                        **kw)
+    for e in (e1, e2, e3):
+        e.reset()
+    rng = np.random.RandomState(0)
+    for t in range(20):
+        a = torch.from_numpy(rng.randint(0, 9, 16).astype(np.int32)).to(dev)
+        p = e1.step(a)[0].cpu().numpy().astype(np.int64)
+        c = e2.step(a)[0].cpu().numpy().astype(np.int64)
+        u = e3.step(a)[0].cpu().numpy().astype(np.int64)
+        assert np.array_equal((c << np.arange(15)).sum(-1), p & 0x7FFF)
+        for k, ch in enumerate((0, 9, 12, 15)):
+            assert np.array_equal(u[..., k], (p >> ch) & 1)
+
+
+def test_reset_roll_augmentation_vs_oracle(torch_dev):
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    path = os.path.join(GOLDEN, "pools", "c3_prune_still_64.npz")
+    levels = _levels_from_pool(path)
+    B, seed = 16, 99
+    venv = SafeLifeVecEnv(LevelPool.load(path), B, "cuda:0", rng="philox", seed=seed,
+                          augment_roll=True, level_order="random", view_shape=(9, 9),
+                          output_channels=None)
+    venv.reset()
+    K = len(levels)
+    for e in range(B):
+        idx = min(int(oracle.philox_uniform(e, 0, 0x5EED, 2, seed) * K), K - 1)
+        dy = min(int(oracle.philox_uniform(e, 0, 0x0011, 3, seed) * 64), 63)
+        dx = min(int(oracle.philox_uniform(e, 0, 0x0022, 3, seed) * 64), 63)
+        lv = levels[idx].rolled(dy, dx)
+        assert venv.state["level_index"][e].item() == idx
+        assert np.array_equal(venv.start_board[e].cpu().numpy(), lv.board)
+        assert np.array_equal(venv.goals[e].cpu().numpy(), lv.goals)
+        assert (venv.state["agent_x"][e].item(), venv.state["agent_y"][e].item()) == lv.agent_loc
