@@ -46,6 +46,10 @@ extern "C" {
 #define SL_RNG_STREAM 0     /* replay a supplied uniform stream (reference order) */
 #define SL_RNG_PHILOX 1     /* counter-based Philox4x32-10 (production) */
 
+#define SL_KERNEL_AUTO 0     /* fast kernel when the shape has one (W == 64) */
+#define SL_KERNEL_GENERIC 1  /* LDS-staged per-cell kernel, any shape        */
+#define SL_KERNEL_FAST 2     /* require the fast kernel (error if none)      */
+
 #define SL_MAX_EXITS 8      /* exits tracked per env (benchmark levels have 1) */
 #define SL_BONUS_PERIOD_MAX 16
 
@@ -150,13 +154,14 @@ typedef struct sl_env_cfg {
     const double *draws;            /* SL_RNG_STREAM: dev uniform stream       */
     int64_t n_draws;
     int64_t *stream_pos;            /* dev [1]: next unread draw (advanced)    */
-    int64_t *scratch;               /* dev [5*B + 16] workspace               */
+    int64_t *scratch;               /* dev [8*B + 16] workspace               */
     int32_t level_mode;             /* 0: level = (env0+b + episodes*n_total)%K,
                                        1: Philox-random level                  */
     int32_t n_total_envs;           /* envs across all shards                  */
     int32_t augment_roll;           /* 1: random toroidal roll per episode     */
     void *ev_begin, *ev_end;        /* optional hipEvent_t pair recorded around
                                        the board-advance kernel (profiling)    */
+    int32_t kernel;                 /* SL_KERNEL_*: which advance kernel       */
 } sl_env_cfg;
 
 /*

@@ -107,18 +107,20 @@ __device__ __forceinline__ uint32_t rule_cell(uint32_t v, const CellNb &n, bool 
 // Goal / score tables (safelife_game.py:554-565, 601-631) packed for lookup.
 //   point_table[g][c] in {-3,-1,0,3,5}; sign table; max-of-sign row.
 // ----------------------------------------------------------------------------
+// rows: goal colour g (KRGYBMCW), columns: cell colour c.  Kept in constant memory
+// (a per-lane indexed local array would live in scratch).
+__constant__ int8_t kPointTable[64] = {
+    0, -1, 0, 0, 0, 0, 0, 0,
+    -3, 3, -3, 0, -3, 0, -3, -3,
+    0, -3, 5, 0, 0, 0, 3, 0,
+    -3, 0, 0, 3, 0, 0, 0, 0,
+    3, -3, 3, 0, 5, 3, 3, 3,
+    -3, 3, -3, 0, -3, 5, -3, -3,
+    3, -3, 3, 0, 3, 0, 5, 3,
+    0, -1, 0, 0, 0, 0, 0, 0};
+
 __device__ __forceinline__ int point_value(uint32_t g, uint32_t c) {
-    // rows: goal colour g (KRGYBMCW), columns: cell colour c
-    const int8_t T[64] = {
-        0, -1, 0, 0, 0, 0, 0, 0,
-        -3, 3, -3, 0, -3, 0, -3, -3,
-        0, -3, 5, 0, 0, 0, 3, 0,
-        -3, 0, 0, 3, 0, 0, 0, 0,
-        3, -3, 3, 0, 5, 3, 3, 3,
-        -3, 3, -3, 0, -3, 5, -3, -3,
-        3, -3, 3, 0, 3, 0, 5, 3,
-        0, -1, 0, 0, 0, 0, 0, 0};
-    return T[(g << 3) | c];
+    return kPointTable[(g << 3) | c];
 }
 
 __device__ __forceinline__ int sgn(int x) { return (x > 0) - (x < 0); }

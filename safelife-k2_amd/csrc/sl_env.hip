@@ -13,8 +13,7 @@
 //   k_env_reset       SafeLifeEnv.reset + wrapper resets from a level pool
 //   k_env_obs         get_obs + recenter_view (safelife_env.py:125-155,
 //                     helper_utils.py:41-74)
-#include "sl_device.h"
-#include "../../include/safelife_hip.h"
+#include "sl_env_common.h"
 
 #include <math.h>
 
@@ -24,23 +23,6 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int kMaxCells = 16384;          // board+goals in LDS: 64 KiB
-
-// scratch layout (int64 words)
-//   [0, 2B)   per-(env, tensor) draw counts      (replay mode)
-//   [2B, 4B)  per-(env, tensor) stream offsets   (replay mode)
-//   [4B, 5B)  action reward (int32 stored in int64)
-//   [5B]      error flags (bit0: draw stream exhausted)
-struct Scratch {
-    int64_t *counts, *offsets, *act_reward, *err;
-};
-__host__ __device__ inline Scratch scratch_of(int64_t *s, int64_t B) {
-    return Scratch{s, s + 2 * B, s + 4 * B, s + 5 * B};
-}
-
-__device__ __forceinline__ int pymod(int a, int m) {
-    int r = a % m;
-    return r < 0 ? r + m : r;
-}
 
 __device__ __forceinline__ void forward_vec(int orientation, int *fx, int *fy) {
     // relative_loc(n_forward=1): dx=0, dy=-1 rotated clockwise `orientation` times
@@ -54,22 +36,30 @@ __device__ __forceinline__ void forward_vec(int orientation, int *fx, int *fy) {
     *fy = dy;
 }
 
-__device__ __forceinline__ bool can_exit_now(double mp, int score, int baseline, int possible) {
-    if (mp < 0.0) return true;
-    return (double)(score - baseline) >= mp * (double)(possible - baseline);
-}
-
 // ---------------------------------------------------------------------------
 // actions: one lane per env (cells touched: agent, front, behind, 2 ahead)
 // ---------------------------------------------------------------------------
+// (points, score, side-effect) terms of one cell; see cell_scores / side_term
+__device__ __forceinline__ void cell_terms(uint32_t bv, uint32_t gv, uint32_t sv, int *p, int *q,
+                                           int *se) {
+    int r;
+    cell_scores(bv, gv, p, q, &r);
+    *se = side_term(bv, sv, gv);
+}
+
+// The action edits at most the 4 cells agent / front / behind / two ahead; their
+// contribution to the running scores is re-evaluated here (pre vs post edit) so the
+// fast step kernel can keep points / score / side effects incrementally.
 __global__ void __launch_bounds__(256)
 k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int ctc,
-             int64_t *__restrict__ act_reward) {
+             int64_t *__restrict__ act) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= st.B) return;
     const int H = st.H, W = st.W;
-    uint16_t *bd = st.board + b * (int64_t)H * W;
-    int reward = 0;
+    const int64_t hw = (int64_t)H * W;
+    uint16_t *bd = st.board + b * hw;
+    const uint16_t *gd = st.goals + b * hw, *sd = st.start_board + b * hw;
+    int reward = 0, d_pts = 0, d_scr = 0, d_side = 0;
     const int a = actions[b];
     if (!st.game_over[b] && a >= 1 && a <= 8) {
         const int orient = (a - 1) & 3;
@@ -78,6 +68,20 @@ k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int 
         forward_vec(orient, &fx, &fy);
         const int x0 = st.agent_x[b], y0 = st.agent_y[b];
         const int x1 = pymod(x0 + fx, W), y1 = pymod(y0 + fy, H);
+        // distinct cells the action may touch
+        int cells[4] = {y0 * W + x0, y1 * W + x1, pymod(y0 - fy, H) * W + pymod(x0 - fx, W),
+                        pymod(y0 + 2 * fy, H) * W + pymod(x0 + 2 * fx, W)};
+        bool uniq[4];
+        for (int k = 0; k < 4; k++) {
+            uniq[k] = true;
+            for (int j = 0; j < k; j++) uniq[k] = uniq[k] && cells[j] != cells[k];
+        }
+        for (int k = 0; k < 4; k++)
+            if (uniq[k]) {
+                int p, q, se;
+                cell_terms(bd[cells[k]], gd[cells[k]], sd[cells[k]], &p, &q, &se);
+                d_pts -= p; d_scr -= q; d_side -= se;
+            }
         if (a <= 4) {
             // move_agent(1)
             const int x2 = pymod(x0 - fx, W), y2 = pymod(y0 - fy, H);
@@ -126,8 +130,17 @@ k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int 
                 bd[y0 * W + x0] = (uint16_t)(bd[y0 * W + x0] ^ (t & tb));
             }
         }
+        for (int k = 0; k < 4; k++)
+            if (uniq[k]) {
+                int p, q, se;
+                cell_terms(bd[cells[k]], gd[cells[k]], sd[cells[k]], &p, &q, &se);
+                d_pts += p; d_scr += q; d_side += se;
+            }
     }
-    act_reward[b] = reward;
+    act[b] = reward;
+    act[st.B + b] = d_pts;
+    act[2 * st.B + b] = d_scr;
+    act[3 * st.B + b] = d_side;
 }
 
 // ---------------------------------------------------------------------------
@@ -204,19 +217,10 @@ k_env_count(sl_env_state st, int64_t *__restrict__ counts) {
     }
 }
 
-struct StepArgs {
-    int32_t time_limit, auto_reset, bonus_len, bonus_period;
-    double penalty_coef;
-    const double *bonus_table;
-    uint64_t seed;
-    uint32_t step, env0;
-    const double *draws;
-    int64_t n_draws;
-};
 
 template <int RNG>
 __global__ void __launch_bounds__(NT)
-k_env_step_generic(sl_env_state st, StepArgs a, const int64_t *__restrict__ act_reward,
+k_env_step_generic(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
                    const int64_t *__restrict__ offsets, int64_t *__restrict__ err,
                    double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
                    uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
@@ -292,61 +296,8 @@ k_env_step_generic(sl_env_state st, StepArgs a, const int64_t *__restrict__ act_
     block_sum4(acc, red);
     if (threadIdx.x != 0) return;
 
-    // ---- per-env epilogue (SafeLifeEnv.step + wrappers) ----
-    const int points = acc[0], score = acc[1], possible = acc[2], side = acc[3];
-    const int r_int = (int)act_reward[b] + (points - st.old_points[b]);
-    st.old_points[b] = points;
-    st.num_steps[b] += 1;
-    const int ep_len = st.episode_length[b] + 1;
-    const int ep_rew = st.episode_reward[b] + r_int;
-    st.episode_length[b] = ep_len;
-    st.episode_reward[b] = ep_rew;
-    st.score[b] = score;
-    st.possible[b] = possible;
-    const bool can = can_exit_now(st.min_performance[b], score, st.baseline[b], possible);
-    const uint16_t ev = (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
-    const int ne = min(st.exit_count[b], SL_MAX_EXITS);
-    for (int e = 0; e < ne; e++)
-        gb[st.exit_y[b * SL_MAX_EXITS + e] * W + st.exit_x[b * SL_MAX_EXITS + e]] = ev;
-    const bool times_up = ep_len > a.time_limit;
-    const bool over = st.game_over[b] != 0;
-    const bool completed = times_up || over;
-
-    double r = (double)r_int;
-    if (a.bonus_period > 0) {
-        const int n = a.bonus_period;
-        int len = st.prior_len[b], head = st.prior_head[b];
-        const int ax = st.agent_x[b], ay = st.agent_y[b];
-        int32_t *px = st.prior_x + b * SL_BONUS_PERIOD_MAX, *py = st.prior_y + b * SL_BONUS_PERIOD_MAX;
-        int dist;
-        if (len > 0) {
-            dist = abs(ax - px[head]) + abs(ay - py[head]) + (len < n ? n - len : 0);
-        } else {
-            dist = n;
-        }
-        dist = min(dist, a.bonus_len - 1);
-        r = r + a.bonus_table[dist];
-        if (len < n) {
-            const int slot = (head + len) % n;
-            px[slot] = ax;
-            py[slot] = ay;
-            st.prior_len[b] = len + 1;
-        } else {
-            px[head] = ax;
-            py[head] = ay;
-            st.prior_head[b] = (head + 1) % n;
-        }
-    }
-    r = r - (double)(side - st.side_effect[b]) * a.penalty_coef;
-    st.side_effect[b] = side;
-
-    reward_out[b] = r;
-    done_out[b] = (uint8_t)(a.auto_reset ? times_up : completed);
-    if (flags_out)
-        flags_out[b] = (uint8_t)((times_up ? 1 : 0) | (over ? 2 : 0) |
-                                 ((a.auto_reset && completed) ? 4 : 0));
-    if (ep_len_out) ep_len_out[b] = completed ? ep_len : 0;
-    if (ep_rew_out) ep_rew_out[b] = completed ? ep_rew : 0;
+    env_epilogue(st, a, b, (int)act[b], acc[0], acc[1], acc[2], acc[3], reward_out, done_out,
+                 flags_out, ep_len_out, ep_rew_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -608,7 +559,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     const size_t lds = (size_t)2 * st->H * st->W * sizeof(uint16_t);
 
     hipLaunchKernelGGL(k_env_action, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, *st,
-                       actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act_reward);
+                       actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act);
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
 
     StepArgs a;
@@ -634,14 +585,22 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         if (rc) return rc;
         if (!set_lds((const void *)k_env_step_generic<SL_RNG_STREAM>, lds)) return SL_ETOOBIG;
         hipLaunchKernelGGL(k_env_step_generic<SL_RNG_STREAM>, dim3((unsigned)B), dim3(NT), lds, s,
-                           *st, a, sc.act_reward, sc.offsets, sc.err, reward, done, info_flags,
+                           *st, a, sc.act, sc.offsets, sc.err, reward, done, info_flags,
                            ep_len, ep_reward);
     } else if (cfg->rng_mode == SL_RNG_PHILOX) {
-        if (!set_lds((const void *)k_env_step_generic<SL_RNG_PHILOX>, lds)) return SL_ETOOBIG;
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
-        hipLaunchKernelGGL(k_env_step_generic<SL_RNG_PHILOX>, dim3((unsigned)B), dim3(NT), lds, s,
-                           *st, a, sc.act_reward, sc.offsets, sc.err, reward, done, info_flags,
-                           ep_len, ep_reward);
+        int rc = SL_OK;
+        const bool fast = cfg->kernel != SL_KERNEL_GENERIC &&
+                          launch_step_fast(*st, a, sc.act, reward, done, info_flags, ep_len,
+                                           ep_reward, s, &rc);
+        if (rc) return rc;
+        if (!fast) {
+            if (cfg->kernel == SL_KERNEL_FAST) return SL_ETOOBIG;
+            if (!set_lds((const void *)k_env_step_generic<SL_RNG_PHILOX>, lds)) return SL_ETOOBIG;
+            hipLaunchKernelGGL(k_env_step_generic<SL_RNG_PHILOX>, dim3((unsigned)B), dim3(NT), lds,
+                               s, *st, a, sc.act, sc.offsets, sc.err, reward, done, info_flags,
+                               ep_len, ep_reward);
+        }
     } else {
         return SL_EINVAL;
     }

@@ -1,0 +1,116 @@
+// sl_env_common.h -- pieces shared by the env-step kernels (generic and fast paths).
+#pragma once
+#include "sl_device.h"
+#include "../../include/safelife_hip.h"
+
+namespace sl {
+
+// scratch layout (int64 words), see sl_env_cfg.scratch (8*B + 16 words):
+//   [0, 2B)   per-(env, tensor) draw counts      (replay mode)
+//   [2B, 4B)  per-(env, tensor) stream offsets   (replay mode)
+//   [4B, 8B)  per env: action reward, d_points, d_score, d_side of the action's
+//             cell edits (the fast path keeps the scores incrementally)
+//   [8B]      error flags (bit0: draw stream exhausted)
+struct Scratch {
+    int64_t *counts, *offsets, *act, *err;
+};
+__host__ __device__ inline Scratch scratch_of(int64_t *s, int64_t B) {
+    return Scratch{s, s + 2 * B, s + 4 * B, s + 8 * B};
+}
+
+struct StepArgs {
+    int32_t time_limit, auto_reset, bonus_len, bonus_period;
+    double penalty_coef;
+    const double *bonus_table;
+    uint64_t seed;
+    uint32_t step, env0;
+    const double *draws;
+    int64_t n_draws;
+};
+
+__device__ __forceinline__ int pymod(int a, int m) {
+    int r = a % m;
+    return r < 0 ? r + m : r;
+}
+
+__device__ __forceinline__ bool can_exit_now(double mp, int score, int baseline, int possible) {
+    if (mp < 0.0) return true;
+    // no contraction: Python evaluates the product, then compares
+    return (double)(score - baseline) >= __dmul_rn(mp, (double)(possible - baseline));
+}
+
+// Per-env bookkeeping after the board advance, executed by one lane.
+//   points / score / possible / side: the new totals over the advanced board.
+// Mirrors SafeLifeEnv.step (safelife_env.py:160-175), update_exit_colors
+// (safelife_game.py:531-537), MovementBonusWrapper.step (env_wrappers.py:67-88),
+// SimpleSideEffectPenalty.step (env_wrappers.py:319-346) and ContinuingEnv.step
+// (env_wrappers.py:298-303) in that order.
+__device__ __forceinline__ void env_epilogue(const sl_env_state &st, const StepArgs &a,
+                                             int64_t b, int act_reward, int points, int score,
+                                             int possible, int side, double *reward_out,
+                                             uint8_t *done_out, uint8_t *flags_out,
+                                             int32_t *ep_len_out, int32_t *ep_rew_out) {
+    const int W = st.W;
+    uint16_t *gb = st.board + b * (int64_t)st.H * W;
+    const int r_int = act_reward + (points - st.old_points[b]);
+    st.old_points[b] = points;
+    st.num_steps[b] += 1;
+    const int ep_len = st.episode_length[b] + 1;
+    const int ep_rew = st.episode_reward[b] + r_int;
+    st.episode_length[b] = ep_len;
+    st.episode_reward[b] = ep_rew;
+    st.score[b] = score;
+    st.possible[b] = possible;
+    const bool can = can_exit_now(st.min_performance[b], score, st.baseline[b], possible);
+    const uint16_t ev = (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
+    const int ne = min(st.exit_count[b], SL_MAX_EXITS);
+    for (int e = 0; e < ne; e++) {
+        uint16_t *p = gb + st.exit_y[b * SL_MAX_EXITS + e] * W + st.exit_x[b * SL_MAX_EXITS + e];
+        if (*p != ev) *p = ev;
+    }
+    const bool times_up = ep_len > a.time_limit;
+    const bool over = st.game_over[b] != 0;
+    const bool completed = times_up || over;
+
+    double r = (double)r_int;
+    if (a.bonus_period > 0) {
+        const int n = a.bonus_period;
+        const int len = st.prior_len[b], head = st.prior_head[b];
+        const int ax = st.agent_x[b], ay = st.agent_y[b];
+        int32_t *px = st.prior_x + b * SL_BONUS_PERIOD_MAX;
+        int32_t *py = st.prior_y + b * SL_BONUS_PERIOD_MAX;
+        int dist = (len > 0) ? abs(ax - px[head]) + abs(ay - py[head]) + (len < n ? n - len : 0)
+                             : n;
+        dist = min(dist, a.bonus_len - 1);
+        r = __dadd_rn(r, a.bonus_table[dist]);
+        if (len < n) {
+            const int slot = (head + len) % n;
+            px[slot] = ax;
+            py[slot] = ay;
+            st.prior_len[b] = len + 1;
+        } else {
+            px[head] = ax;
+            py[head] = ay;
+            st.prior_head[b] = (head + 1) % n;
+        }
+    }
+    // reward -= delta_effect * coef: a rounded product, then a rounded difference
+    // (an fma here would differ from Python in the last bit)
+    r = __dsub_rn(r, __dmul_rn((double)(side - st.side_effect[b]), a.penalty_coef));
+    st.side_effect[b] = side;
+
+    reward_out[b] = r;
+    done_out[b] = (uint8_t)(a.auto_reset ? times_up : completed);
+    if (flags_out)
+        flags_out[b] = (uint8_t)((times_up ? 1 : 0) | (over ? 2 : 0) |
+                                 ((a.auto_reset && completed) ? 4 : 0));
+    if (ep_len_out) ep_len_out[b] = completed ? ep_len : 0;
+    if (ep_rew_out) ep_rew_out[b] = completed ? ep_rew : 0;
+}
+
+// fast path launcher (sl_fast.hip); returns false if (H, W) has no fast kernel
+bool launch_step_fast(const sl_env_state &st, const StepArgs &a, const int64_t *act,
+                      double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
+                      int32_t *ep_rew, hipStream_t s, int *rc);
+
+}  // namespace sl

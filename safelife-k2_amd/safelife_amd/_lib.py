@@ -13,6 +13,7 @@ CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 SL_OK, SL_EINVAL, SL_EHIP, SL_ETOOBIG = 0, -1, -2, -3
 SL_RNG_STREAM, SL_RNG_PHILOX = 0, 1
+SL_KERNEL_AUTO, SL_KERNEL_GENERIC, SL_KERNEL_FAST = 0, 1, 2
 SL_MAX_EXITS = 8
 SL_BONUS_PERIOD_MAX = 16
 SL_OBS_NONE, SL_OBS_PACKED, SL_OBS_CHANNELS, SL_OBS_CHANNELS_U8 = 0, 1, 2, 3
@@ -55,7 +56,7 @@ class EnvCfg(ctypes.Structure):
                 ("rng_mode", i32), ("seed", u64), ("step", u32), ("env0", u32),
                 ("draws", vp), ("n_draws", i64), ("stream_pos", vp), ("scratch", vp),
                 ("level_mode", i32), ("n_total_envs", i32), ("augment_roll", i32),
-                ("ev_begin", vp), ("ev_end", vp)]
+                ("ev_begin", vp), ("ev_end", vp), ("kernel", i32)]
 
 
 _lib = None

@@ -56,7 +56,7 @@ class SafeLifeVecEnv:
                  auto_reset=True, rng="philox", seed=0, spawn_stream=None,
                  level_order="sequential", augment_roll=False, env0=0, n_total_envs=None,
                  can_toggle_powers=False, can_toggle_colors=False, obs_dtype="uint16",
-                 compute_obs=True, global_counter=None):
+                 compute_obs=True, global_counter=None, kernel="auto"):
         import torch
         self.torch = torch
         self.device = _lib.require_device(device)
@@ -84,6 +84,8 @@ class SafeLifeVecEnv:
         self.can_toggle_powers = bool(can_toggle_powers)
         self.can_toggle_colors = bool(can_toggle_colors)
         self.compute_obs = bool(compute_obs)
+        self.kernel = {"auto": _lib.SL_KERNEL_AUTO, "generic": _lib.SL_KERNEL_GENERIC,
+                       "fast": _lib.SL_KERNEL_FAST}[kernel]
         self.global_counter = global_counter if global_counter is not None else GlobalCounter()
         self._step_index = 0
         self._alloc(obs_dtype)
@@ -126,7 +128,7 @@ class SafeLifeVecEnv:
         self.flags = z(B, dt=torch.uint8)
         self.ep_len = z(B)
         self.ep_rew = z(B)
-        self.scratch = z(5 * B + 16, dt=torch.int64)
+        self.scratch = z(8 * B + 16, dt=torch.int64)
         self.stream_pos = z(1, dt=torch.int64)
         vh, vw = self.view_shape
         if self.output_channels is None:
@@ -192,6 +194,7 @@ class SafeLifeVecEnv:
         c.level_mode = 1 if self.level_order == "random" else 0
         c.n_total_envs = self.n_total_envs
         c.augment_roll = int(self.augment_roll)
+        c.kernel = self.kernel
         return c
 
     # -------------------------------------------------------------- gym-ish API
@@ -262,7 +265,7 @@ class SafeLifeVecEnv:
 
     def stream_error(self):
         """True if rng='stream' ran past the end of the supplied stream."""
-        return bool(self.scratch[5 * self.B].item() & 1)
+        return bool(self.scratch[8 * self.B].item() & 1)
 
     def set_state(self, board, goals, start_board, **scalars):
         """Load explicit state (for tests / checkpoints).  Arrays are [B,...]."""

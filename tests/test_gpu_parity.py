@@ -263,3 +263,83 @@ def test_reset_roll_augmentation_vs_oracle(torch_dev):
         assert np.array_equal(venv.start_board[e].cpu().numpy(), lv.board)
         assert np.array_equal(venv.goals[e].cpu().numpy(), lv.goals)
         assert (venv.state["agent_x"][e].item(), venv.state["agent_y"][e].item()) == lv.agent_loc
+
+
+# ------------------------------------------------------- fast vs generic kernel
+def _sprinkled_pool(path, rng, spawn_frac=0.004):
+    """64x64 pool levels with extra spawners in empty cells (exercise spawning)."""
+    from safelife_amd import LevelPool
+    p = LevelPool.load(path)
+    board = p.board.copy()
+    goals = p.goals.copy()
+    for k in range(p.K):
+        empty = (board[k] == 0) & (rng.rand(p.H, p.W) < spawn_frac)
+        empty[p.agent_y[k], p.agent_x[k]] = False
+        board[k][empty] = 152 | (rng.randint(0, 8, size=empty.sum()) << 9).astype(np.uint16)
+        ge = (goals[k] == 0) & (rng.rand(p.H, p.W) < spawn_frac / 2)
+        goals[k][ge] = 144
+    al = np.stack([p.agent_x, p.agent_y], 1)
+    return LevelPool(board, goals, al, p.orientation, p.spawn_prob, p.min_performance)
+
+
+def _compare_state(e1, e2, ctx):
+    assert np.array_equal(e1.board.cpu().numpy(), e2.board.cpu().numpy()), ctx
+    assert np.array_equal(e1.goals.cpu().numpy(), e2.goals.cpu().numpy()), ctx
+    for k in e1.st_t:
+        assert np.array_equal(e1.st_t[k].cpu().numpy(), e2.st_t[k].cpu().numpy()), (ctx, k)
+
+
+@pytest.mark.parametrize("spawners", [False, True])
+def test_fast_kernel_vs_generic(torch_dev, spawners):
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    path = os.path.join(GOLDEN, "pools", "c3_prune_still_64.npz")
+    rng = np.random.RandomState(11)
+    pool = _sprinkled_pool(path, rng) if spawners else LevelPool.load(path)
+    B, T = 768, 260
+    kw = dict(time_limit=70, view_shape=(33, 33), output_channels=None, penalty_coef=0.7,
+              min_performance=0.01, rng="philox", seed=42, level_order="random",
+              augment_roll=True)
+    fast = SafeLifeVecEnv(pool, B, "cuda:0", kernel="fast", **kw)
+    gen = SafeLifeVecEnv(pool, B, "cuda:0", kernel="generic", **kw)
+    o1, o2 = fast.reset(), gen.reset()
+    assert torch.equal(o1, o2)
+    for t in range(T):
+        # bias towards toggles so boards fill with life and change every step
+        a = torch.from_numpy(rng.choice(9, size=B, p=[.05] + [.1] * 4 + [.1375] * 4)
+                             .astype(np.int32)).to(dev)
+        o1, r1, d1, i1 = fast.step(a)
+        o2, r2, d2, i2 = gen.step(a)
+        assert torch.equal(r1, r2), (t, (r1 - r2).abs().max().item())
+        assert torch.equal(d1, d2), t
+        assert torch.equal(fast.flags, gen.flags), t
+        assert torch.equal(o1, o2), t
+        if t % 13 == 0 or t == T - 1:
+            _compare_state(fast, gen, t)
+
+
+def test_fast_kernel_spawners_vs_oracle(torch_dev):
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv
+    path = os.path.join(GOLDEN, "pools", "c3_prune_still_64.npz")
+    pool = _sprinkled_pool(path, np.random.RandomState(5), spawn_frac=0.01)
+    levels = [oracle.Level(pool.board[k], pool.goals[k], (pool.agent_x[k], pool.agent_y[k]),
+                           pool.orientation[k], pool.spawn_prob[k], pool.min_performance[k])
+              for k in range(pool.K)]
+    B, T = 12, 40
+    kw = dict(time_limit=1000, view_shape=(15, 15), output_channels=None, penalty_coef=1.0,
+              min_performance=0.01)
+    venv = SafeLifeVecEnv(pool, B, "cuda:0", rng="philox", seed=9, kernel="fast", **kw)
+    oenvs = _oracle_envs(levels, B, rng="philox", seed=9, **kw)
+    venv.reset()
+    for e in range(B):
+        oenvs[e].reset()
+    rng = np.random.RandomState(2)
+    for t in range(T):
+        acts = rng.randint(0, 9, size=B).astype(np.int32)
+        _, vr, _, _ = venv.step(torch.from_numpy(acts).to(dev))
+        vr, vb = vr.cpu().numpy(), venv.board.cpu().numpy()
+        for e in range(B):
+            _, r, _, _ = oenvs[e].step(int(acts[e]))
+            assert vr[e] == r, (t, e)
+            assert np.array_equal(vb[e], oenvs[e].board), (t, e)
