@@ -31,6 +31,13 @@ namespace {
 
 constexpr uint32_t ONE2 = 0x00010001u;
 
+#ifndef SL_FAST_UNR
+#define SL_FAST_UNR 4      // rows per unrolled chunk of the 16-row strip
+#endif
+#ifndef SL_FAST_OCC
+#define SL_FAST_OCC 3      // waves per SIMD the register budget is sized for
+#endif
+
 __device__ __forceinline__ uint32_t pk_shr(uint32_t val, uint32_t amt) {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
     us2 v = __builtin_bit_cast(us2, val), s = __builtin_bit_cast(us2, amt);
@@ -119,40 +126,70 @@ __device__ __forceinline__ uint32_t decide(uint32_t v, const CW &w, uint32_t oU,
     return out;
 }
 
-__device__ __forceinline__ uint32_t apply_spawn(uint32_t out, uint32_t elig, uint32_t spv,
-                                                int cell0, uint32_t gid, const StepArgs &a,
-                                                uint32_t tensor, double thr) {
-    if (elig & 1u) {
-        if (philox_uniform((uint32_t)cell0, gid, a.step, tensor, a.seed) < thr)
-            out = (out & 0xFFFF0000u) | (spv & 0xFFFFu);
+// -- cold paths, kept out of line so the unrolled hot loop stays small ----------
+
+// spawn draws for one row (board pair 0/1, goal pair 0/1); rare: only rows where a
+// cell next to a spawner is eligible
+__device__ __forceinline__ uint4 spawn_row(uint4 o, uint4 e, uint4 sv, int cell, uint32_t gid,
+                                        uint32_t step, uint64_t seed, double thr) {
+    uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+    const uint32_t ew[4] = {e.x, e.y, e.z, e.w}, sw[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {           // q: 0,1 board pairs; 2,3 goal pairs
+        const uint32_t tensor = q >> 1;
+        const int c0 = cell + 2 * (q & 1);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            if ((ew[q] >> (16 * h)) & 1u) {
+                if (philox_uniform((uint32_t)(c0 + h), gid, step, tensor, seed) < thr) {
+                    const uint32_t m = 0xFFFFu << (16 * h);
+                    ow[q] = (ow[q] & ~m) | (sw[q] & m);
+                }
+            }
+        }
     }
-    if (elig & 0x10000u) {
-        if (philox_uniform((uint32_t)cell0 + 1u, gid, a.step, tensor, a.seed) < thr)
-            out = (out & 0x0000FFFFu) | (spv & 0xFFFF0000u);
-    }
-    return out;
+    return make_uint4(ow[0], ow[1], ow[2], ow[3]);
 }
 
-__device__ __forceinline__ void delta_cell(uint32_t ob, uint32_t nb, uint32_t og, uint32_t ng,
-                                           uint32_t s, int d[4]) {
-    if (ob == nb && og == ng) return;
-    int p0, q0, r0, p1, q1, r1;
-    cell_scores(ob, og, &p0, &q0, &r0);
-    cell_scores(nb, ng, &p1, &q1, &r1);
-    d[0] += p1 - p0;
-    d[1] += q1 - q0;
-    d[2] += r1 - r0;
-    d[3] += side_term(nb, s, ng) - side_term(ob, s, og);
+// score deltas of the 4 cells of a row that changed (board and/or goals)
+__device__ __forceinline__ int4 delta_row(uint2 ob, uint2 nb, uint2 og, uint2 ng, uint2 s) {
+    const uint32_t obw[2] = {ob.x, ob.y}, nbw[2] = {nb.x, nb.y};
+    const uint32_t ogw[2] = {og.x, og.y}, ngw[2] = {ng.x, ng.y}, sw[2] = {s.x, s.y};
+    int d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int sh = 16 * h;
+            const uint32_t o = (obw[j] >> sh) & 0xFFFF, n = (nbw[j] >> sh) & 0xFFFF;
+            const uint32_t go = (ogw[j] >> sh) & 0xFFFF, gn = (ngw[j] >> sh) & 0xFFFF;
+            const uint32_t sv = (sw[j] >> sh) & 0xFFFF;
+            if (o == n && go == gn) continue;
+            int p0, q0, r0, p1, q1, r1;
+            cell_scores(o, go, &p0, &q0, &r0);
+            cell_scores(n, gn, &p1, &q1, &r1);
+            d0 += p1 - p0;
+            d1 += q1 - q0;
+            d2 += r1 - r0;
+            d3 += side_term(n, sv, gn) - side_term(o, sv, go);
+        }
+    return make_int4(d0, d1, d2, d3);
 }
 
-template <int H>
-__global__ void __launch_bounds__(256, 3)
+__device__ __forceinline__ int wrap_row(int y, int H) { return y < 0 ? y + H : (y >= H ? y - H : y); }
+
+// H: board height (W = 64); UNR: rows per unrolled chunk (divides H/4); the next
+// chunk's rows are prefetched while the current chunk is computed.
+template <int H, int UNR>
+__global__ void __launch_bounds__(256, SL_FAST_OCC)
 k_env_step_w64(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
                double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
                uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
                int32_t *__restrict__ ep_rew_out) {
     constexpr int R = H / 4;           // rows per strip
     constexpr int RW = 16;             // uint2 words per row
+    constexpr int NCH = R / UNR;
+    static_assert(R % UNR == 0, "UNR must divide the strip height");
     const int lane = threadIdx.x & 63;
     const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= st.B) return;             // whole wave leaves together
@@ -163,76 +200,107 @@ k_env_step_w64(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
     uint2 *gg = reinterpret_cast<uint2 *>(st.goals + off);
     const uint2 *gs = reinterpret_cast<const uint2 *>(st.start_board + off);
 
-    uint2 vb[R + 2], vg[R + 2];
+    // rows y0-1 and y0 (halo + first centre), then the first chunk of "next" rows
+    const uint2 hb = gb[wrap_row(y0 - 1, H) * RW + cg], hg = gg[wrap_row(y0 - 1, H) * RW + cg];
+    uint2 vb = gb[y0 * RW + cg], vg = gg[y0 * RW + cg];
+    uint2 nxb[UNR], nxg[UNR];
 #pragma unroll
-    for (int k = 0; k < R + 2; k++) {
-        int y = y0 - 1 + k;
-        y = y < 0 ? y + H : (y >= H ? y - H : y);
-        vb[k] = gb[y * RW + cg];
-        vg[k] = gg[y * RW + cg];
+    for (int j = 0; j < UNR; j++) {
+        const int y = wrap_row(y0 + 1 + j, H);
+        nxb[j] = gb[y * RW + cg];
+        nxg[j] = gg[y * RW + cg];
     }
-    uint32_t sp_b = 0, sp_g = 0;
+    // any spawner on the board / goals: the whole strip group must agree, so test
+    // every row once up front (cheap: one OR per row word, one ballot)
+    uint32_t spb = hb.x | hb.y | vb.x | vb.y, spg = hg.x | hg.y | vg.x | vg.y;
 #pragma unroll
-    for (int k = 1; k <= R; k++) {
-        sp_b |= vb[k].x | vb[k].y;
-        sp_g |= vg[k].x | vg[k].y;
+    for (int j = 0; j < UNR; j++) {
+        spb |= nxb[j].x | nxb[j].y;
+        spg |= nxg[j].x | nxg[j].y;
     }
-    const bool spawn_b = __ballot((sp_b & 0x00800080u) != 0) != 0;   // any spawner: board
-    const bool spawn_g = __ballot((sp_g & 0x00800080u) != 0) != 0;   //              goals
+    if (NCH > 1) {
+        // rows beyond the first chunk: test them too (they are re-read later from L2)
+#pragma unroll 4
+        for (int k = UNR + 1; k < R; k++) {
+            const uint2 xb = gb[(y0 + k) * RW + cg], xg = gg[(y0 + k) * RW + cg];
+            spb |= xb.x | xb.y;
+            spg |= xg.x | xg.y;
+        }
+    }
+    const bool spawn_b = __ballot((spb & 0x00800080u) != 0) != 0;
+    const bool spawn_g = __ballot((spg & 0x00800080u) != 0) != 0;
     const double thr = (double)st.spawn_prob[b];
     const uint32_t gid = a.env0 + (uint32_t)b;
 
-    CW wb0 = cword(vb[0].x, spawn_b), wb1 = cword(vb[0].y, spawn_b);
-    CW wg0 = cword(vg[0].x, spawn_g), wg1 = cword(vg[0].y, spawn_g);
+    CW wb0 = cword(hb.x, spawn_b), wb1 = cword(hb.y, spawn_b);
+    CW wg0 = cword(hg.x, spawn_g), wg1 = cword(hg.y, spawn_g);
     RowSum pb = row_sum(wb0.c, wb1.c), pg = row_sum(wg0.c, wg1.c);
-    wb0 = cword(vb[1].x, spawn_b); wb1 = cword(vb[1].y, spawn_b);
-    wg0 = cword(vg[1].x, spawn_g); wg1 = cword(vg[1].y, spawn_g);
+    wb0 = cword(vb.x, spawn_b); wb1 = cword(vb.y, spawn_b);
+    wg0 = cword(vg.x, spawn_g); wg1 = cword(vg.y, spawn_g);
     RowSum cb = row_sum(wb0.c, wb1.c), cgs = row_sum(wg0.c, wg1.c);
 
     int d[4] = {0, 0, 0, 0};           // d points, d score, d possible, d side
-#pragma clang loop unroll(full)
-    for (int r = 0; r < R; r++) {
-        const int k = r + 1;
-        const int y = y0 + r;
-        const CW nb0w = cword(vb[k + 1].x, spawn_b), nb1w = cword(vb[k + 1].y, spawn_b);
-        const CW ng0w = cword(vg[k + 1].x, spawn_g), ng1w = cword(vg[k + 1].y, spawn_g);
-        const RowSum nbs = row_sum(nb0w.c, nb1w.c), ngs = row_sum(ng0w.c, ng1w.c);
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ch++) {
+        uint2 pfb[UNR], pfg[UNR];
+        if (ch + 1 < NCH) {
+#pragma unroll
+            for (int j = 0; j < UNR; j++) {
+                const int y = wrap_row(y0 + (ch + 1) * UNR + 1 + j, H);
+                pfb[j] = gb[y * RW + cg];
+                pfg[j] = gg[y * RW + cg];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UNR; j++) {
+            const int y = y0 + ch * UNR + j;           // centre row
+            const CW nb0w = cword(nxb[j].x, spawn_b), nb1w = cword(nxb[j].y, spawn_b);
+            const CW ng0w = cword(nxg[j].x, spawn_g), ng1w = cword(nxg[j].y, spawn_g);
+            const RowSum nbs = row_sum(nb0w.c, nb1w.c), ngs = row_sum(ng0w.c, ng1w.c);
 
-        uint32_t eb0, eb1, eg0, eg1, sb0, sb1, sg0, sg1;
-        uint32_t b0 = decide(vb[k].x, wb0, pb.o0, pb.t0, pb.n0, cb.o0, cb.t0, cb.n0, nbs.o0,
-                             nbs.t0, nbs.n0, spawn_b, &eb0, &sb0);
-        uint32_t b1 = decide(vb[k].y, wb1, pb.o1, pb.t1, pb.n1, cb.o1, cb.t1, cb.n1, nbs.o1,
-                             nbs.t1, nbs.n1, spawn_b, &eb1, &sb1);
-        uint32_t g0 = decide(vg[k].x, wg0, pg.o0, pg.t0, pg.n0, cgs.o0, cgs.t0, cgs.n0, ngs.o0,
-                             ngs.t0, ngs.n0, spawn_g, &eg0, &sg0);
-        uint32_t g1 = decide(vg[k].y, wg1, pg.o1, pg.t1, pg.n1, cgs.o1, cgs.t1, cgs.n1, ngs.o1,
-                             ngs.t1, ngs.n1, spawn_g, &eg1, &sg1);
-        if (spawn_b || spawn_g) {
-            if (__ballot((eb0 | eb1 | eg0 | eg1) != 0)) {
-                const int cell = y * 64 + cg * 4;
-                b0 = apply_spawn(b0, eb0, sb0, cell, gid, a, 0u, thr);
-                b1 = apply_spawn(b1, eb1, sb1, cell + 2, gid, a, 0u, thr);
-                g0 = apply_spawn(g0, eg0, sg0, cell, gid, a, 1u, thr);
-                g1 = apply_spawn(g1, eg1, sg1, cell + 2, gid, a, 1u, thr);
+            uint32_t o[4], e[4], sv[4];
+            o[0] = decide(vb.x, wb0, pb.o0, pb.t0, pb.n0, cb.o0, cb.t0, cb.n0, nbs.o0, nbs.t0,
+                          nbs.n0, spawn_b, &e[0], &sv[0]);
+            o[1] = decide(vb.y, wb1, pb.o1, pb.t1, pb.n1, cb.o1, cb.t1, cb.n1, nbs.o1, nbs.t1,
+                          nbs.n1, spawn_b, &e[1], &sv[1]);
+            o[2] = decide(vg.x, wg0, pg.o0, pg.t0, pg.n0, cgs.o0, cgs.t0, cgs.n0, ngs.o0, ngs.t0,
+                          ngs.n0, spawn_g, &e[2], &sv[2]);
+            o[3] = decide(vg.y, wg1, pg.o1, pg.t1, pg.n1, cgs.o1, cgs.t1, cgs.n1, ngs.o1, ngs.t1,
+                          ngs.n1, spawn_g, &e[3], &sv[3]);
+            if (spawn_b || spawn_g) {
+                const bool any_e = (e[0] | e[1] | e[2] | e[3]) != 0;
+                if (__ballot(any_e)) {
+                    if (any_e) {
+                        const uint4 r4 = spawn_row(make_uint4(o[0], o[1], o[2], o[3]),
+                                                   make_uint4(e[0], e[1], e[2], e[3]),
+                                                   make_uint4(sv[0], sv[1], sv[2], sv[3]),
+                                                   y * 64 + cg * 4, gid, a.step, a.seed, thr);
+                        o[0] = r4.x; o[1] = r4.y; o[2] = r4.z; o[3] = r4.w;
+                    }
+                }
+            }
+            const bool chb = ((o[0] ^ vb.x) | (o[1] ^ vb.y)) != 0;
+            const bool chg = ((o[2] ^ vg.x) | (o[3] ^ vg.y)) != 0;
+            if (__ballot(chb || chg)) {
+                if (chb) gb[y * RW + cg] = make_uint2(o[0], o[1]);
+                if (chg) gg[y * RW + cg] = make_uint2(o[2], o[3]);
+                if (chb || chg) {
+                    const int4 dd = delta_row(vb, make_uint2(o[0], o[1]), vg,
+                                              make_uint2(o[2], o[3]), gs[y * RW + cg]);
+                    d[0] += dd.x; d[1] += dd.y; d[2] += dd.z; d[3] += dd.w;
+                }
+            }
+            pb = cb; cb = nbs; pg = cgs; cgs = ngs;
+            wb0 = nb0w; wb1 = nb1w; wg0 = ng0w; wg1 = ng1w;
+            vb = nxb[j]; vg = nxg[j];
+        }
+        if (ch + 1 < NCH) {
+#pragma unroll
+            for (int j = 0; j < UNR; j++) {
+                nxb[j] = pfb[j];
+                nxg[j] = pfg[j];
             }
         }
-        const bool chb = ((b0 ^ vb[k].x) | (b1 ^ vb[k].y)) != 0;
-        const bool chg = ((g0 ^ vg[k].x) | (g1 ^ vg[k].y)) != 0;
-        if (__ballot(chb || chg)) {
-            if (chb) gb[y * RW + cg] = make_uint2(b0, b1);
-            if (chg) gg[y * RW + cg] = make_uint2(g0, g1);
-            if (chb || chg) {
-                const uint2 s = gs[y * RW + cg];
-                delta_cell(vb[k].x & 0xFFFF, b0 & 0xFFFF, vg[k].x & 0xFFFF, g0 & 0xFFFF,
-                           s.x & 0xFFFF, d);
-                delta_cell(vb[k].x >> 16, b0 >> 16, vg[k].x >> 16, g0 >> 16, s.x >> 16, d);
-                delta_cell(vb[k].y & 0xFFFF, b1 & 0xFFFF, vg[k].y & 0xFFFF, g1 & 0xFFFF,
-                           s.y & 0xFFFF, d);
-                delta_cell(vb[k].y >> 16, b1 >> 16, vg[k].y >> 16, g1 >> 16, s.y >> 16, d);
-            }
-        }
-        pb = cb; cb = nbs; pg = cgs; cgs = ngs;
-        wb0 = nb0w; wb1 = nb1w; wg0 = ng0w; wg1 = ng1w;
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) d[q] = wave_sum(d[q]);
@@ -258,8 +326,8 @@ bool launch_step_fast(const sl_env_state &st, const StepArgs &a, const int64_t *
     const unsigned grid = (unsigned)((st.B + 3) / 4);
     switch (st.H) {
         case 64:
-            hipLaunchKernelGGL(k_env_step_w64<64>, dim3(grid), dim3(256), 0, s, st, a, act, reward,
-                               done, flags, ep_len, ep_rew);
+            hipLaunchKernelGGL((k_env_step_w64<64, SL_FAST_UNR>), dim3(grid), dim3(256), 0, s, st,
+                               a, act, reward, done, flags, ep_len, ep_rew);
             break;
         default:
             return false;

@@ -8,7 +8,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_native", "libsafelife_hip.so")
+LIB_PATH = os.environ.get("SAFELIFE_HIP_LIB") or os.path.join(_HERE, "_native",
+                                                              "libsafelife_hip.so")
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 SL_OK, SL_EINVAL, SL_EHIP, SL_ETOOBIG = 0, -1, -2, -3
