@@ -32,10 +32,10 @@ namespace {
 constexpr uint32_t ONE2 = 0x00010001u;
 
 #ifndef SL_FAST_UNR
-#define SL_FAST_UNR 4      // rows per unrolled chunk of the 16-row strip
+#define SL_FAST_UNR 2      // rows per unrolled chunk of the 16-row strip
 #endif
 #ifndef SL_FAST_OCC
-#define SL_FAST_OCC 3      // waves per SIMD the register budget is sized for
+#define SL_FAST_OCC 4      // waves per SIMD the register budget is sized for
 #endif
 
 __device__ __forceinline__ uint32_t pk_shr(uint32_t val, uint32_t amt) {
@@ -203,16 +203,25 @@ k_env_step_w64(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
     // rows y0-1 and y0 (halo + first centre), then the first chunk of "next" rows
     const uint2 hb = gb[wrap_row(y0 - 1, H) * RW + cg], hg = gg[wrap_row(y0 - 1, H) * RW + cg];
     uint2 vb = gb[y0 * RW + cg], vg = gg[y0 * RW + cg];
+    // the bottom halo row is the next strip's first row, which that strip (the same
+    // wave) overwrites in its first chunk: read it before any store
+    const int ybot = wrap_row(y0 + R, H);
+    const uint2 tb = gb[ybot * RW + cg], tg = gg[ybot * RW + cg];
     uint2 nxb[UNR], nxg[UNR];
 #pragma unroll
     for (int j = 0; j < UNR; j++) {
-        const int y = wrap_row(y0 + 1 + j, H);
-        nxb[j] = gb[y * RW + cg];
-        nxg[j] = gg[y * RW + cg];
+        if (1 + j < R) {
+            nxb[j] = gb[(y0 + 1 + j) * RW + cg];
+            nxg[j] = gg[(y0 + 1 + j) * RW + cg];
+        } else {
+            nxb[j] = tb;
+            nxg[j] = tg;
+        }
     }
     // any spawner on the board / goals: the whole strip group must agree, so test
     // every row once up front (cheap: one OR per row word, one ballot)
-    uint32_t spb = hb.x | hb.y | vb.x | vb.y, spg = hg.x | hg.y | vg.x | vg.y;
+    uint32_t spb = hb.x | hb.y | vb.x | vb.y | tb.x | tb.y;
+    uint32_t spg = hg.x | hg.y | vg.x | vg.y | tg.x | tg.y;
 #pragma unroll
     for (int j = 0; j < UNR; j++) {
         spb |= nxb[j].x | nxb[j].y;
@@ -246,9 +255,14 @@ k_env_step_w64(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
         if (ch + 1 < NCH) {
 #pragma unroll
             for (int j = 0; j < UNR; j++) {
-                const int y = wrap_row(y0 + (ch + 1) * UNR + 1 + j, H);
-                pfb[j] = gb[y * RW + cg];
-                pfg[j] = gg[y * RW + cg];
+                const int k = (ch + 1) * UNR + 1 + j;          // strip-relative row
+                if (k < R) {
+                    pfb[j] = gb[(y0 + k) * RW + cg];
+                    pfg[j] = gg[(y0 + k) * RW + cg];
+                } else {
+                    pfb[j] = tb;
+                    pfg[j] = tg;
+                }
             }
         }
 #pragma unroll
