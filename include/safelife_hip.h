@@ -123,6 +123,9 @@ typedef struct sl_env_state {
     int32_t *level_index;     /* level of the current episode                 */
     int32_t *episodes;        /* episodes started by this env                 */
     int32_t *num_steps;       /* game.num_steps                               */
+    int32_t *spawn_flags;     /* bit0: board, bit1: goals hold a spawning cell
+                                 (set at reset; spawning bits are never created
+                                 by the rule or the actions, only moved)       */
 } sl_env_state;
 
 /* A device-resident level pool (the level_iterator's levels). */

@@ -304,6 +304,7 @@ k_env_step_generic(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
 // reset from the level pool
 // ---------------------------------------------------------------------------
 struct ResetArgs {
+    int32_t toggle_powers;
     double wrapper_min_perf;
     uint64_t seed;
     uint32_t env0;
@@ -311,16 +312,19 @@ struct ResetArgs {
     int32_t bonus_period;
 };
 
-__global__ void __launch_bounds__(NT)
-k_env_reset(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ mask,
-            const uint8_t *__restrict__ flags, ResetArgs a) {
-    __shared__ int red[NT / 64][4];
-    __shared__ int wave_tot[NT / 64];
-    __shared__ int sh_exit_y[SL_MAX_EXITS], sh_exit_x[SL_MAX_EXITS];
-    __shared__ int sh_ev, sh_idx, sh_dy, sh_dx;
-    const int64_t b = blockIdx.x;
-    if (mask && !mask[b]) return;
-    if (flags && !(flags[b] & 4)) return;
+struct ResetShared {
+    int red[NT / 64][4];
+    int wave_tot[NT / 64];
+    int exit_y[SL_MAX_EXITS], exit_x[SL_MAX_EXITS];
+    int ev, idx, dy, dx;
+};
+
+__device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &a,
+                          int64_t b, ResetShared &sh) {
+    int (*red)[4] = sh.red;
+    int *wave_tot = sh.wave_tot;
+    int *sh_exit_y = sh.exit_y, *sh_exit_x = sh.exit_x;
+    int &sh_ev = sh.ev, &sh_idx = sh.idx, &sh_dy = sh.dy, &sh_dx = sh.dx;
     const int H = st.H, W = st.W, hw = H * W;
     const uint32_t gid = a.env0 + (uint32_t)b;
     if (threadIdx.x == 0) {
@@ -346,7 +350,7 @@ k_env_reset(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ mas
     const uint16_t *pb = pool.board + (int64_t)idx * hw, *pg = pool.goals + (int64_t)idx * hw;
 
     // pass 1: reductions + ordered exit list of the (rolled) initial board
-    int acc[4] = {0, 0, 0, 0};   // points, score(=baseline), possible, exits
+    int acc[4] = {0, 0, 0, 0};   // points, score(=baseline), possible, spawn flags
     int n_exit = 0;
     const int nchunk = (hw + NT - 1) / NT;
     for (int c = 0; c < nchunk; c++) {
@@ -361,6 +365,7 @@ k_env_reset(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ mas
             acc[0] += p;
             acc[1] += q;
             acc[2] += r;
+            acc[3] += ((vb & SPAWN) ? 1 : 0) + ((vg & SPAWN) ? 65536 : 0);  // counts < 2^16
             ex = (vb & EXIT) != 0;
         }
         int tot;
@@ -383,6 +388,8 @@ k_env_reset(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ mas
         st.orientation[b] = pool.orientation[idx];
         st.game_over[b] = 0;
         st.num_steps[b] = 0;
+        st.spawn_flags[b] = ((acc[3] & 0xFFFF) || a.toggle_powers ? 1 : 0) |
+                            ((acc[3] >> 16) ? 2 : 0);
         st.episode_length[b] = 0;
         st.episode_reward[b] = 0;
         st.old_points[b] = points;
@@ -414,6 +421,19 @@ k_env_reset(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ mas
         gs[i] = vb;
         gb[i] = (vb & EXIT) ? ev : vb;
         gg[i] = pg[src];
+    }
+}
+
+// grid-stride over envs: cheap when only a few envs reset this step
+__global__ void __launch_bounds__(NT)
+k_env_reset(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ mask,
+            const uint8_t *__restrict__ flags, ResetArgs a) {
+    __shared__ ResetShared sh;
+    for (int64_t b = blockIdx.x; b < st.B; b += gridDim.x) {
+        if (mask && !mask[b]) continue;
+        if (flags && !(flags[b] & 4)) continue;
+        reset_one(st, pool, a, b, sh);
+        __syncthreads();
     }
 }
 
@@ -481,6 +501,8 @@ bool set_lds(const void *fn, size_t bytes) {
            hipSuccess;
 }
 
+unsigned reset_grid(int64_t B) { return (unsigned)(B < 2048 ? B : 2048); }
+
 bool state_ok(const sl_env_state *st) {
     return st && st->B >= 0 && st->H >= 2 && st->W >= 2 && st->board && st->goals &&
            st->start_board && (int64_t)st->H * st->W <= kMaxCells;
@@ -495,6 +517,7 @@ ResetArgs reset_args(const sl_env_cfg *cfg) {
     r.n_total = cfg->n_total_envs > 0 ? cfg->n_total_envs : 1;
     r.augment = cfg->augment_roll;
     r.bonus_period = cfg->bonus_period;
+    r.toggle_powers = cfg->can_toggle_powers;
     return r;
 }
 
@@ -539,7 +562,7 @@ extern "C" int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const u
     if (!state_ok(st) || !pool || !cfg || pool->K <= 0 || pool->H != st->H || pool->W != st->W)
         return SL_EINVAL;
     if (st->B == 0) return SL_OK;
-    hipLaunchKernelGGL(k_env_reset, dim3((unsigned)st->B), dim3(NT), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_env_reset, dim3(reset_grid(st->B)), dim3(NT), 0, (hipStream_t)stream,
                        *st, *pool, mask, (const uint8_t *)nullptr, reset_args(cfg));
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
@@ -558,10 +581,6 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     Scratch sc = scratch_of(cfg->scratch, B);
     const size_t lds = (size_t)2 * st->H * st->W * sizeof(uint16_t);
 
-    hipLaunchKernelGGL(k_env_action, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, *st,
-                       actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act);
-    if (hipGetLastError() != hipSuccess) return SL_EHIP;
-
     StepArgs a;
     a.time_limit = cfg->time_limit;
     a.auto_reset = cfg->auto_reset;
@@ -575,40 +594,45 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     a.draws = cfg->draws;
     a.n_draws = cfg->n_draws;
 
-    if (cfg->rng_mode == SL_RNG_STREAM) {
-        if (!cfg->stream_pos || (!cfg->draws && cfg->n_draws > 0)) return SL_EINVAL;
-        if (!set_lds((const void *)k_env_count, lds)) return SL_ETOOBIG;
-        hipLaunchKernelGGL(k_env_count, dim3((unsigned)B), dim3(NT), lds, s, *st, sc.counts);
-        if (hipGetLastError() != hipSuccess) return SL_EHIP;
-        int rc = sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * B, cfg->stream_pos,
-                                       cfg->stream_pos, stream);
-        if (rc) return rc;
-        if (!set_lds((const void *)k_env_step_generic<SL_RNG_STREAM>, lds)) return SL_ETOOBIG;
-        hipLaunchKernelGGL(k_env_step_generic<SL_RNG_STREAM>, dim3((unsigned)B), dim3(NT), lds, s,
-                           *st, a, sc.act, sc.offsets, sc.err, reward, done, info_flags,
-                           ep_len, ep_reward);
-    } else if (cfg->rng_mode == SL_RNG_PHILOX) {
+    const bool fast = cfg->rng_mode == SL_RNG_PHILOX && cfg->kernel != SL_KERNEL_GENERIC &&
+                      fast_shape(st->H, st->W);
+    if (cfg->kernel == SL_KERNEL_FAST && !fast) return SL_ETOOBIG;
+    if (fast) {
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
-        int rc = SL_OK;
-        const bool fast = cfg->kernel != SL_KERNEL_GENERIC &&
-                          launch_step_fast(*st, a, sc.act, reward, done, info_flags, ep_len,
-                                           ep_reward, s, &rc);
+        int rc = launch_step_fast(*st, a, actions, cfg->can_toggle_powers, cfg->can_toggle_colors,
+                                  reward, done, info_flags, ep_len, ep_reward, s);
         if (rc) return rc;
-        if (!fast) {
-            if (cfg->kernel == SL_KERNEL_FAST) return SL_ETOOBIG;
+    } else {
+        hipLaunchKernelGGL(k_env_action, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, *st,
+                           actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act);
+        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        if (cfg->rng_mode == SL_RNG_STREAM) {
+            if (!cfg->stream_pos || (!cfg->draws && cfg->n_draws > 0)) return SL_EINVAL;
+            if (!set_lds((const void *)k_env_count, lds)) return SL_ETOOBIG;
+            hipLaunchKernelGGL(k_env_count, dim3((unsigned)B), dim3(NT), lds, s, *st, sc.counts);
+            if (hipGetLastError() != hipSuccess) return SL_EHIP;
+            int rc = sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * B, cfg->stream_pos,
+                                           cfg->stream_pos, stream);
+            if (rc) return rc;
+            if (!set_lds((const void *)k_env_step_generic<SL_RNG_STREAM>, lds)) return SL_ETOOBIG;
+            hipLaunchKernelGGL(k_env_step_generic<SL_RNG_STREAM>, dim3((unsigned)B), dim3(NT), lds,
+                               s, *st, a, sc.act, sc.offsets, sc.err, reward, done, info_flags,
+                               ep_len, ep_reward);
+        } else if (cfg->rng_mode == SL_RNG_PHILOX) {
             if (!set_lds((const void *)k_env_step_generic<SL_RNG_PHILOX>, lds)) return SL_ETOOBIG;
+            if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
             hipLaunchKernelGGL(k_env_step_generic<SL_RNG_PHILOX>, dim3((unsigned)B), dim3(NT), lds,
                                s, *st, a, sc.act, sc.offsets, sc.err, reward, done, info_flags,
                                ep_len, ep_reward);
+        } else {
+            return SL_EINVAL;
         }
-    } else {
-        return SL_EINVAL;
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (cfg->ev_end) (void)hipEventRecord((hipEvent_t)cfg->ev_end, s);
 
     if (cfg->auto_reset) {
-        hipLaunchKernelGGL(k_env_reset, dim3((unsigned)B), dim3(NT), 0, s, *st, *pool,
+        hipLaunchKernelGGL(k_env_reset, dim3(reset_grid(B)), dim3(NT), 0, s, *st, *pool,
                            (const uint8_t *)nullptr, (const uint8_t *)info_flags,
                            reset_args(cfg));
         if (hipGetLastError() != hipSuccess) return SL_EHIP;

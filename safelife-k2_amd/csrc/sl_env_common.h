@@ -108,9 +108,10 @@ __device__ __forceinline__ void env_epilogue(const sl_env_state &st, const StepA
     if (ep_rew_out) ep_rew_out[b] = completed ? ep_rew : 0;
 }
 
-// fast path launcher (sl_fast.hip); returns false if (H, W) has no fast kernel
-bool launch_step_fast(const sl_env_state &st, const StepArgs &a, const int64_t *act,
-                      double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
-                      int32_t *ep_rew, hipStream_t s, int *rc);
+// fused fast path (sl_fast.hip): action + advance + scores in one kernel
+bool fast_shape(int H, int W);
+int launch_step_fast(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
+                     int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
+                     int32_t *ep_rew, hipStream_t s);
 
 }  // namespace sl

@@ -1,28 +1,36 @@
-// sl_fast.hip -- the env-step kernel for 64-wide boards (the headline 64x64 config).
+// sl_fast.hip -- the fused env-step kernel for 64-wide boards (the headline 64x64 config).
 //
-// Same semantics as k_env_step_generic (sl_env.hip), re-laid-out for CDNA4:
+// Same semantics as k_env_action + k_env_step_generic (sl_env.hip), re-laid-out
+// for CDNA4:
 //
-//  * one wave64 per env, four envs per 256-thread workgroup, no LDS, no barriers;
+//  * one wave64 per env, four envs per 256-thread workgroup, no barriers after
+//    the prologue;
+//  * the action (execute_action / move_agent, safelife_game.py:308-393) is
+//    evaluated by lane 0 against an overlay of at most 4 cells and broadcast as
+//    uniform (row, column, value) edits that every lane applies to the rows it
+//    loads -- the row loads are in flight while lane 0 works;
 //  * lane = (strip, column group): 16 lanes span a 64-cell row (4 cells = 8 bytes
 //    each, so a wave-wide load is four fully-used 128-byte row segments) and the 4
 //    strips of 16 lanes each own H/4 consecutive rows;
 //  * a row's 4 cells live packed two per 32-bit register (two uint16 halves), so
-//    every bitwise op, v_alignbit, v_pk_lshrrev_b16 and v_mul_u32_u24 below
+//    every bitwise op, v_bitop3, v_perm, v_pk_lshrrev_b16 and v_mul_u32_u24 below
 //    evaluates the rule for 2 cells at once;
 //  * horizontal neighbours: the 16-lane DPP rotations row_ror:1 / row_ror:15 wrap
 //    exactly at W = 64 (the torus), so the left / right neighbour words cost one
-//    DPP move each and three v_alignbit funnel shifts;
+//    DPP move each and three funnel shifts;
 //  * vertical neighbours: each lane walks its strip top to bottom with a rolling
-//    window of row summaries (the two halo rows are re-read from L2);
+//    window of row summaries; rows are fetched UNR at a time, one chunk ahead;
 //  * each row summary folds the 3 cells of a row into ones (OR), twos (>= 2,
 //    majority) and a count; the column pass folds 3 row summaries the same way
-//    (reference advance_board.c:12-32,51-86 does the same
-//    separable fold cell by cell);
+//    (the reference's advance_board.c:12-32,51-86 does the
+//    same separable fold cell by cell);
+//  * spawner code lives in a second copy of the row loop and only runs for envs
+//    whose level holds a spawning cell (sl_env_state.spawn_flags);
 //  * scores are kept incrementally: points / perf score / possible / side-effect
-//    totals change only where a cell changed, so the per-cell scoring work, the
-//    start-board read and the store are all skipped (wave-uniformly) on rows
-//    where nothing changed -- on still-life boards almost every row.
-//    The totals equal the full sums the generic kernel computes (tested).
+//    totals change only where a cell changed, so the per-cell scoring work (an
+//    LDS table lookup), the start-board read and the store are all skipped
+//    (wave-uniformly) on rows where nothing changed.  The totals equal the full
+//    sums the generic kernel computes (tests: test_fast_kernel_vs_generic).
 #include "sl_env_common.h"
 
 using namespace sl;
@@ -45,7 +53,7 @@ __device__ __forceinline__ uint32_t pk_shr(uint32_t val, uint32_t amt) {
 }
 
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
-    return (m & x) | (~m & y);                            // v_bfi_b32
+    return (m & x) | (~m & y);                            // v_bfi_b32 / v_bitop3
 }
 
 // 0xFFFF in every 16-bit half whose bit 0 (bit 16) is set: x is 0/1 per half
@@ -53,25 +61,26 @@ __device__ __forceinline__ uint32_t expand(uint32_t x) { return __umul24(x, 0xFF
 
 // lane (l - 1) mod 16 / (l + 1) mod 16 inside each 16-lane DPP row
 __device__ __forceinline__ uint32_t from_left(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x121, 0xF, 0xF, false);
 }
 __device__ __forceinline__ uint32_t from_right(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12F, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x12F, 0xF, 0xF, false);
 }
 
 struct CW {          // contribution words of a row pair-register
     uint32_t c, a, am;
 };
 
-// c(n) per cell (see sl_device.h): P|I|S flags, alive destructible-or-exit +
+// c(n) per cell (see sl_device.h): alive, P|I|S flags, alive destructible-or-exit +
 // colours at bits 8-11, spawner colours at bits 13-15.
-__device__ __forceinline__ CW cword(uint32_t v, bool spawn) {
+template <bool SPAWN>
+__device__ __forceinline__ CW cword(uint32_t v) {
     CW r;
     r.a = v & ONE2;
     r.am = expand(r.a);
     const uint32_t t = ((v << 5) & 0x01000100u) | v;       // exit bit |= destructible
-    uint32_t c = ((t & 0x0F000F00u) & r.am) | (v & 0x00E000E0u) | r.a;
-    if (spawn) {
+    uint32_t c = ((t & 0x0F000F00u) & r.am) | (v & 0x00E100E1u);
+    if (SPAWN) {
         const uint32_t sm = expand((v >> 7) & ONE2);
         c |= ((v & 0x0E000E00u) << 4) & sm;
     }
@@ -103,9 +112,10 @@ __device__ __forceinline__ RowSum row_sum(uint32_t c0, uint32_t c1) {
 // rule for one pair-register given the folded neighbourhood.
 //   returns the new pair; *elig = per-half bit 0 set where the cell draws a uniform;
 //   *spv = the value a spawn would write (per half).
+template <bool SPAWN>
 __device__ __forceinline__ uint32_t decide(uint32_t v, const CW &w, uint32_t oU, uint32_t tU,
                                            uint32_t nU, uint32_t oC, uint32_t tC, uint32_t nC,
-                                           uint32_t oD, uint32_t tD, uint32_t nD, bool spawn,
+                                           uint32_t oD, uint32_t tD, uint32_t nD,
                                            uint32_t *elig, uint32_t *spv) {
     const uint32_t ones = oU | oC | oD;
     const uint32_t twos = tU | tC | tD | bfi(oU ^ oC, oD, oU);
@@ -117,45 +127,51 @@ __device__ __forceinline__ uint32_t decide(uint32_t v, const CW &w, uint32_t oU,
     const uint32_t cols = (twos | (ones >> 4)) & 0x0E000E00u;
     const uint32_t bv = cols | ((twos >> 5) & 0x00080008u) | ONE2;   // newborn
     const uint32_t out = bfi(expand(change), bfi(w.am, 0u, bv), v);
-    if (spawn) {
+    if (SPAWN) {
         *elig = (ones >> 7) & ~(hold | x | w.a) & ONE2;
         *spv = cols | 0x00090009u;
     } else {
         *elig = 0;
+        *spv = 0;
     }
     return out;
 }
 
-// -- cold paths, kept out of line so the unrolled hot loop stays small ----------
+__device__ __forceinline__ uint32_t spawn_pair(uint32_t o, uint32_t e, uint32_t sv, int cell,
+                                               uint32_t gid, uint32_t step, uint32_t tensor,
+                                               uint64_t seed, double thr) {
+    if (e & 1u)
+        if (philox_uniform((uint32_t)cell, gid, step, tensor, seed) < thr)
+            o = (o & 0xFFFF0000u) | (sv & 0xFFFFu);
+    if (e & 0x10000u)
+        if (philox_uniform((uint32_t)cell + 1u, gid, step, tensor, seed) < thr)
+            o = (o & 0x0000FFFFu) | (sv & 0xFFFF0000u);
+    return o;
+}
 
-// spawn draws for one row (board pair 0/1, goal pair 0/1); rare: only rows where a
-// cell next to a spawner is eligible
-__device__ __forceinline__ uint4 spawn_row(uint4 o, uint4 e, uint4 sv, int cell, uint32_t gid,
-                                        uint32_t step, uint64_t seed, double thr) {
-    uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-    const uint32_t ew[4] = {e.x, e.y, e.z, e.w}, sw[4] = {sv.x, sv.y, sv.z, sv.w};
-#pragma unroll
-    for (int q = 0; q < 4; q++) {           // q: 0,1 board pairs; 2,3 goal pairs
-        const uint32_t tensor = q >> 1;
-        const int c0 = cell + 2 * (q & 1);
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            if ((ew[q] >> (16 * h)) & 1u) {
-                if (philox_uniform((uint32_t)(c0 + h), gid, step, tensor, seed) < thr) {
-                    const uint32_t m = 0xFFFFu << (16 * h);
-                    ow[q] = (ow[q] & ~m) | (sw[q] & m);
-                }
-            }
-        }
-    }
-    return make_uint4(ow[0], ow[1], ow[2], ow[3]);
+// ---------------------------------------------------------------- scoring
+// LDS lookup table, index (goal colour << 3) | cell colour:
+//   bits 0-3: point_table + 3, bits 4-5: sign(point_table) + 1, bit 6: max(sign row)
+struct ScoreTbl {
+    uint16_t e[64];
+};
+
+__device__ __forceinline__ void cell_terms_lds(const ScoreTbl &tb, uint32_t b, uint32_t g,
+                                               uint32_t s, int *p, int *q, int *r, int *se) {
+    const uint32_t e = tb.e[((g >> 6) & 0x38u) | ((b >> 9) & 7u)];
+    const bool alive = b & ALIVE;
+    const bool m = alive && ((b & (FROZEN | MOVABLE)) != FROZEN);
+    *p = alive ? (int)(e & 15u) - 3 : 0;
+    *q = m ? (int)((e >> 4) & 3u) - 1 : 0;
+    *r = (int)((e >> 6) & 1u);
+    *se = side_term(b, s, g);
 }
 
 // score deltas of the 4 cells of a row that changed (board and/or goals)
-__device__ __forceinline__ int4 delta_row(uint2 ob, uint2 nb, uint2 og, uint2 ng, uint2 s) {
+__device__ __forceinline__ void delta_row(const ScoreTbl &tb, uint2 ob, uint2 nb, uint2 og,
+                                          uint2 ng, uint2 s, int d[4]) {
     const uint32_t obw[2] = {ob.x, ob.y}, nbw[2] = {nb.x, nb.y};
     const uint32_t ogw[2] = {og.x, og.y}, ngw[2] = {ng.x, ng.y}, sw[2] = {s.x, s.y};
-    int d0 = 0, d1 = 0, d2 = 0, d3 = 0;
 #pragma unroll
     for (int j = 0; j < 2; j++)
 #pragma unroll
@@ -164,91 +180,179 @@ __device__ __forceinline__ int4 delta_row(uint2 ob, uint2 nb, uint2 og, uint2 ng
             const uint32_t o = (obw[j] >> sh) & 0xFFFF, n = (nbw[j] >> sh) & 0xFFFF;
             const uint32_t go = (ogw[j] >> sh) & 0xFFFF, gn = (ngw[j] >> sh) & 0xFFFF;
             const uint32_t sv = (sw[j] >> sh) & 0xFFFF;
-            if (o == n && go == gn) continue;
-            int p0, q0, r0, p1, q1, r1;
-            cell_scores(o, go, &p0, &q0, &r0);
-            cell_scores(n, gn, &p1, &q1, &r1);
-            d0 += p1 - p0;
-            d1 += q1 - q0;
-            d2 += r1 - r0;
-            d3 += side_term(n, sv, gn) - side_term(o, sv, go);
+            if (o != n || go != gn) {
+                int p0, q0, r0, e0, p1, q1, r1, e1;
+                cell_terms_lds(tb, o, go, sv, &p0, &q0, &r0, &e0);
+                cell_terms_lds(tb, n, gn, sv, &p1, &q1, &r1, &e1);
+                d[0] += p1 - p0;
+                d[1] += q1 - q0;
+                d[2] += r1 - r0;
+                d[3] += e1 - e0;
+            }
         }
-    return make_int4(d0, d1, d2, d3);
+}
+
+// ---------------------------------------------------------------- action
+// execute_action / move_agent (safelife_game.py:308-393) on a 4-cell overlay of
+// the board.  Run by one lane; produces the cell edits, the action reward and
+// the score deltas of the edited cells.
+struct Overlay {
+    int n;
+    int idx[4];
+    uint32_t val[4];
+    const uint16_t *bd;
+    __device__ uint32_t get(int i) const {
+        for (int k = 0; k < n; k++)
+            if (idx[k] == i) return val[k];
+        return bd[i];
+    }
+    __device__ void set(int i, uint32_t v) {
+        for (int k = 0; k < n; k++)
+            if (idx[k] == i) {
+                val[k] = v;
+                return;
+            }
+        idx[n] = i;
+        val[n] = v;
+        n++;
+    }
+};
+
+struct ActResult {
+    int reward, dp, dq, dse;
+};
+
+__device__ __forceinline__ int pm(int a, int m) {
+    int r = a % m;
+    return r < 0 ? r + m : r;
+}
+
+__device__ ActResult lane_action(const sl_env_state &st, int64_t b, int a, int ctp, int ctc,
+                                 const ScoreTbl &tb, Overlay &ov) {
+    const int H = st.H, W = st.W;
+    const int64_t hw = (int64_t)H * W;
+    const uint16_t *gd = st.goals + b * hw, *sd = st.start_board + b * hw;
+    ActResult res{0, 0, 0, 0};
+    ov.n = 0;
+    if (st.game_over[b] || a < 1 || a > 8) return res;
+    const int orient = (a - 1) & 3;
+    st.orientation[b] = orient;
+    const int fx = orient == 1 ? 1 : (orient == 3 ? -1 : 0);
+    const int fy = orient == 0 ? -1 : (orient == 2 ? 1 : 0);
+    const int x0 = st.agent_x[b], y0 = st.agent_y[b];
+    const int x1 = pm(x0 + fx, W), y1 = pm(y0 + fy, H);
+    const int i0 = y0 * W + x0, i1 = y1 * W + x1;
+    if (a <= 4) {
+        const int i2 = pm(y0 - fy, H) * W + pm(x0 - fx, W);
+        int nx = x0, ny = y0;
+        const uint32_t c1 = ov.get(i1);
+        if (c1 == 0) {
+            ov.set(i1, ov.get(i0));
+            ov.set(i0, 0);
+            nx = x1; ny = y1;
+        } else if ((c1 & EXIT) &&
+                   can_exit_now(st.min_performance[b], st.score[b], st.baseline[b],
+                                st.possible[b])) {
+            st.game_over[b] = 1;
+            res.reward = 1;
+        } else if (c1 & PUSHABLE) {
+            const int i3 = pm(y0 + 2 * fy, H) * W + pm(x0 + 2 * fx, W);
+            const uint32_t c3 = ov.get(i3);
+            if (c3 == 0) {
+                ov.set(i3, ov.get(i1));
+                ov.set(i1, ov.get(i0));
+                ov.set(i0, 0);
+                nx = x1; ny = y1;
+            } else if (c3 & EXIT) {
+                ov.set(i1, ov.get(i0));
+                ov.set(i0, 0);
+                nx = x1; ny = y1;
+            }
+        }
+        const bool moved = (nx == x1 && ny == y1) && !(x0 == x1 && y0 == y1);
+        if (moved && (ov.get(i2) & PULLABLE)) {
+            ov.set(i0, ov.get(i2));
+            ov.set(i2, 0);
+        }
+        st.agent_x[b] = nx;
+        st.agent_y[b] = ny;
+    } else {
+        const uint32_t pc = ov.get(i0) & COLORS;
+        const uint32_t t = ov.get(i1);
+        if (t == 0) {
+            ov.set(i1, LIFE | pc);
+        } else if (t & DESTR) {
+            ov.set(i1, 0);
+        } else {
+            const uint32_t tbits = (ctp ? POWERS : 0u) | (ctc ? COLORS : 0u);
+            ov.set(i0, ov.get(i0) ^ (t & tbits));
+        }
+    }
+    for (int k = 0; k < ov.n; k++) {
+        const int i = ov.idx[k];
+        int p0, q0, r0, e0, p1, q1, r1, e1;
+        cell_terms_lds(tb, ov.bd[i], gd[i], sd[i], &p0, &q0, &r0, &e0);
+        cell_terms_lds(tb, ov.val[k], gd[i], sd[i], &p1, &q1, &r1, &e1);
+        res.dp += p1 - p0;
+        res.dq += q1 - q0;
+        res.dse += e1 - e0;
+    }
+    return res;
 }
 
 __device__ __forceinline__ int wrap_row(int y, int H) { return y < 0 ? y + H : (y >= H ? y - H : y); }
 
-// H: board height (W = 64); UNR: rows per unrolled chunk (divides H/4); the next
-// chunk's rows are prefetched while the current chunk is computed.
-template <int H, int UNR>
-__global__ void __launch_bounds__(256, SL_FAST_OCC)
-k_env_step_w64(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
-               double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
-               uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
-               int32_t *__restrict__ ep_rew_out) {
-    constexpr int R = H / 4;           // rows per strip
-    constexpr int RW = 16;             // uint2 words per row
-    constexpr int NCH = R / UNR;
-    static_assert(R % UNR == 0, "UNR must divide the strip height");
-    const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b >= st.B) return;             // whole wave leaves together
-    const int cg = lane & 15;
-    const int y0 = (lane >> 4) * R;
-    const int64_t off = b * (int64_t)(H * 64);
-    uint2 *gb = reinterpret_cast<uint2 *>(st.board + off);
-    uint2 *gg = reinterpret_cast<uint2 *>(st.goals + off);
-    const uint2 *gs = reinterpret_cast<const uint2 *>(st.start_board + off);
+// uniform cell edits broadcast from lane 0
+struct Edits {
+    int n;
+    int y[4], cg[4], sh[4], j[4];
+    uint32_t v[4];
+    uint32_t rowmask;    // strip-relative row slots (0 .. R+1) that hold an edit
+};
 
-    // rows y0-1 and y0 (halo + first centre), then the first chunk of "next" rows
-    const uint2 hb = gb[wrap_row(y0 - 1, H) * RW + cg], hg = gg[wrap_row(y0 - 1, H) * RW + cg];
-    uint2 vb = gb[y0 * RW + cg], vg = gg[y0 * RW + cg];
-    // the bottom halo row is the next strip's first row, which that strip (the same
-    // wave) overwrites in its first chunk: read it before any store
-    const int ybot = wrap_row(y0 + R, H);
-    const uint2 tb = gb[ybot * RW + cg], tg = gg[ybot * RW + cg];
-    uint2 nxb[UNR], nxg[UNR];
-#pragma unroll
-    for (int j = 0; j < UNR; j++) {
-        if (1 + j < R) {
-            nxb[j] = gb[(y0 + 1 + j) * RW + cg];
-            nxg[j] = gg[(y0 + 1 + j) * RW + cg];
-        } else {
-            nxb[j] = tb;
-            nxg[j] = tg;
+__device__ __forceinline__ uint2 patch(uint2 w, int y, int cg, const Edits &ed) {
+    for (int k = 0; k < ed.n; k++) {
+        if (y == ed.y[k] && cg == ed.cg[k]) {
+            const uint32_t m = 0xFFFFu << ed.sh[k], nv = ed.v[k] << ed.sh[k];
+            if (ed.j[k]) w.y = (w.y & ~m) | nv;
+            else w.x = (w.x & ~m) | nv;
         }
     }
-    // any spawner on the board / goals: the whole strip group must agree, so test
-    // every row once up front (cheap: one OR per row word, one ballot)
-    uint32_t spb = hb.x | hb.y | vb.x | vb.y | tb.x | tb.y;
-    uint32_t spg = hg.x | hg.y | vg.x | vg.y | tg.x | tg.y;
-#pragma unroll
-    for (int j = 0; j < UNR; j++) {
-        spb |= nxb[j].x | nxb[j].y;
-        spg |= nxg[j].x | nxg[j].y;
-    }
-    if (NCH > 1) {
-        // rows beyond the first chunk: test them too (they are re-read later from L2)
-#pragma unroll 4
-        for (int k = UNR + 1; k < R; k++) {
-            const uint2 xb = gb[(y0 + k) * RW + cg], xg = gg[(y0 + k) * RW + cg];
-            spb |= xb.x | xb.y;
-            spg |= xg.x | xg.y;
-        }
-    }
-    const bool spawn_b = __ballot((spb & 0x00800080u) != 0) != 0;
-    const bool spawn_g = __ballot((spg & 0x00800080u) != 0) != 0;
-    const double thr = (double)st.spawn_prob[b];
-    const uint32_t gid = a.env0 + (uint32_t)b;
+    return w;
+}
 
-    CW wb0 = cword(hb.x, spawn_b), wb1 = cword(hb.y, spawn_b);
-    CW wg0 = cword(hg.x, spawn_g), wg1 = cword(hg.y, spawn_g);
+__device__ __forceinline__ bool has_edit(int y, int cg, const Edits &ed) {
+    bool h = false;
+    for (int k = 0; k < ed.n; k++) h |= (y == ed.y[k] && cg == ed.cg[k]);
+    return h;
+}
+
+// ---------------------------------------------------------------- row loop
+struct Ctx {
+    uint2 *gb, *gg;
+    const uint2 *gs;
+    int cg, y0;
+    uint32_t gid, step;
+    uint64_t seed;
+    double thr;
+};
+
+template <int H, int UNR, bool SPAWN>
+__device__ __forceinline__ void strip_loop(const Ctx &c, const Edits &ed, const ScoreTbl &tb,
+                                           uint2 hb, uint2 hg, uint2 vb, uint2 vg, uint2 tb2,
+                                           uint2 tg2, uint2 (&nxb)[UNR], uint2 (&nxg)[UNR],
+                                           int d[4]) {
+    constexpr int R = H / 4, RW = 16, NCH = R / UNR;
+    const int cg = c.cg, y0 = c.y0;
+    if (ed.rowmask & 1u) hb = patch(hb, wrap_row(y0 - 1, H), cg, ed);
+    if (ed.rowmask & 2u) vb = patch(vb, y0, cg, ed);
+    CW wb0 = cword<SPAWN>(hb.x), wb1 = cword<SPAWN>(hb.y);
+    CW wg0 = cword<SPAWN>(hg.x), wg1 = cword<SPAWN>(hg.y);
     RowSum pb = row_sum(wb0.c, wb1.c), pg = row_sum(wg0.c, wg1.c);
-    wb0 = cword(vb.x, spawn_b); wb1 = cword(vb.y, spawn_b);
-    wg0 = cword(vg.x, spawn_g); wg1 = cword(vg.y, spawn_g);
+    wb0 = cword<SPAWN>(vb.x); wb1 = cword<SPAWN>(vb.y);
+    wg0 = cword<SPAWN>(vg.x); wg1 = cword<SPAWN>(vg.y);
     RowSum cb = row_sum(wb0.c, wb1.c), cgs = row_sum(wg0.c, wg1.c);
 
-    int d[4] = {0, 0, 0, 0};           // d points, d score, d possible, d side
 #pragma unroll 1
     for (int ch = 0; ch < NCH; ch++) {
         uint2 pfb[UNR], pfg[UNR];
@@ -257,56 +361,61 @@ k_env_step_w64(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
             for (int j = 0; j < UNR; j++) {
                 const int k = (ch + 1) * UNR + 1 + j;          // strip-relative row
                 if (k < R) {
-                    pfb[j] = gb[(y0 + k) * RW + cg];
-                    pfg[j] = gg[(y0 + k) * RW + cg];
+                    pfb[j] = c.gb[(y0 + k) * RW + cg];
+                    pfg[j] = c.gg[(y0 + k) * RW + cg];
                 } else {
-                    pfb[j] = tb;
-                    pfg[j] = tg;
+                    pfb[j] = tb2;
+                    pfg[j] = tg2;
                 }
             }
         }
 #pragma unroll
         for (int j = 0; j < UNR; j++) {
-            const int y = y0 + ch * UNR + j;           // centre row
-            const CW nb0w = cword(nxb[j].x, spawn_b), nb1w = cword(nxb[j].y, spawn_b);
-            const CW ng0w = cword(nxg[j].x, spawn_g), ng1w = cword(nxg[j].y, spawn_g);
+            const int r = ch * UNR + j;
+            const int y = y0 + r;                              // centre row
+            uint2 nb = nxb[j];
+            if ((ed.rowmask >> (r + 2)) & 1u) nb = patch(nb, wrap_row(y + 1, H), cg, ed);
+            const uint2 ng = nxg[j];
+            const CW nb0w = cword<SPAWN>(nb.x), nb1w = cword<SPAWN>(nb.y);
+            const CW ng0w = cword<SPAWN>(ng.x), ng1w = cword<SPAWN>(ng.y);
             const RowSum nbs = row_sum(nb0w.c, nb1w.c), ngs = row_sum(ng0w.c, ng1w.c);
 
-            uint32_t o[4], e[4], sv[4];
-            o[0] = decide(vb.x, wb0, pb.o0, pb.t0, pb.n0, cb.o0, cb.t0, cb.n0, nbs.o0, nbs.t0,
-                          nbs.n0, spawn_b, &e[0], &sv[0]);
-            o[1] = decide(vb.y, wb1, pb.o1, pb.t1, pb.n1, cb.o1, cb.t1, cb.n1, nbs.o1, nbs.t1,
-                          nbs.n1, spawn_b, &e[1], &sv[1]);
-            o[2] = decide(vg.x, wg0, pg.o0, pg.t0, pg.n0, cgs.o0, cgs.t0, cgs.n0, ngs.o0, ngs.t0,
-                          ngs.n0, spawn_g, &e[2], &sv[2]);
-            o[3] = decide(vg.y, wg1, pg.o1, pg.t1, pg.n1, cgs.o1, cgs.t1, cgs.n1, ngs.o1, ngs.t1,
-                          ngs.n1, spawn_g, &e[3], &sv[3]);
-            if (spawn_b || spawn_g) {
-                const bool any_e = (e[0] | e[1] | e[2] | e[3]) != 0;
+            uint32_t e0, e1, e2, e3, s0, s1, s2, s3;
+            uint32_t o0 = decide<SPAWN>(vb.x, wb0, pb.o0, pb.t0, pb.n0, cb.o0, cb.t0, cb.n0,
+                                        nbs.o0, nbs.t0, nbs.n0, &e0, &s0);
+            uint32_t o1 = decide<SPAWN>(vb.y, wb1, pb.o1, pb.t1, pb.n1, cb.o1, cb.t1, cb.n1,
+                                        nbs.o1, nbs.t1, nbs.n1, &e1, &s1);
+            uint32_t o2 = decide<SPAWN>(vg.x, wg0, pg.o0, pg.t0, pg.n0, cgs.o0, cgs.t0, cgs.n0,
+                                        ngs.o0, ngs.t0, ngs.n0, &e2, &s2);
+            uint32_t o3 = decide<SPAWN>(vg.y, wg1, pg.o1, pg.t1, pg.n1, cgs.o1, cgs.t1, cgs.n1,
+                                        ngs.o1, ngs.t1, ngs.n1, &e3, &s3);
+            if (SPAWN) {
+                const bool any_e = (e0 | e1 | e2 | e3) != 0;
                 if (__ballot(any_e)) {
                     if (any_e) {
-                        const uint4 r4 = spawn_row(make_uint4(o[0], o[1], o[2], o[3]),
-                                                   make_uint4(e[0], e[1], e[2], e[3]),
-                                                   make_uint4(sv[0], sv[1], sv[2], sv[3]),
-                                                   y * 64 + cg * 4, gid, a.step, a.seed, thr);
-                        o[0] = r4.x; o[1] = r4.y; o[2] = r4.z; o[3] = r4.w;
+                        const int cell = y * 64 + cg * 4;
+                        o0 = spawn_pair(o0, e0, s0, cell, c.gid, c.step, 0u, c.seed, c.thr);
+                        o1 = spawn_pair(o1, e1, s1, cell + 2, c.gid, c.step, 0u, c.seed, c.thr);
+                        o2 = spawn_pair(o2, e2, s2, cell, c.gid, c.step, 1u, c.seed, c.thr);
+                        o3 = spawn_pair(o3, e3, s3, cell + 2, c.gid, c.step, 1u, c.seed, c.thr);
                     }
                 }
             }
-            const bool chb = ((o[0] ^ vb.x) | (o[1] ^ vb.y)) != 0;
-            const bool chg = ((o[2] ^ vg.x) | (o[3] ^ vg.y)) != 0;
-            if (__ballot(chb || chg)) {
-                if (chb) gb[y * RW + cg] = make_uint2(o[0], o[1]);
-                if (chg) gg[y * RW + cg] = make_uint2(o[2], o[3]);
-                if (chb || chg) {
-                    const int4 dd = delta_row(vb, make_uint2(o[0], o[1]), vg,
-                                              make_uint2(o[2], o[3]), gs[y * RW + cg]);
-                    d[0] += dd.x; d[1] += dd.y; d[2] += dd.z; d[3] += dd.w;
-                }
+            // vb carries the action's edits; memory still holds the pre-action row, so
+            // a row with an edit is written back even if the advance kept it
+            const bool sc_b = ((o0 ^ vb.x) | (o1 ^ vb.y)) != 0;
+            const bool sc_g = ((o2 ^ vg.x) | (o3 ^ vg.y)) != 0;
+            const bool edited = ((ed.rowmask >> (r + 1)) & 1u) && has_edit(y, cg, ed);
+            if (__ballot(sc_b || sc_g || edited)) {
+                if (sc_b || edited) c.gb[y * RW + cg] = make_uint2(o0, o1);
+                if (sc_g) c.gg[y * RW + cg] = make_uint2(o2, o3);
+                if (sc_b || sc_g)
+                    delta_row(tb, vb, make_uint2(o0, o1), vg, make_uint2(o2, o3),
+                              c.gs[y * RW + cg], d);
             }
             pb = cb; cb = nbs; pg = cgs; cgs = ngs;
             wb0 = nb0w; wb1 = nb1w; wg0 = ng0w; wg1 = ng1w;
-            vb = nxb[j]; vg = nxg[j];
+            vb = nb; vg = ng;
         }
         if (ch + 1 < NCH) {
 #pragma unroll
@@ -316,15 +425,102 @@ k_env_step_w64(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
             }
         }
     }
+}
+
+// H: board height (W = 64); UNR: rows per unrolled chunk (divides H/4)
+template <int H, int UNR>
+__global__ void __launch_bounds__(256, SL_FAST_OCC)
+k_env_step_w64(sl_env_state st, StepArgs a, const int32_t *__restrict__ actions, int ctp,
+               int ctc, double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
+               uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
+               int32_t *__restrict__ ep_rew_out) {
+    constexpr int R = H / 4;           // rows per strip
+    constexpr int RW = 16;             // uint2 words per row
+    static_assert(R % UNR == 0, "UNR must divide the strip height");
+    __shared__ ScoreTbl tbl;
+    if (threadIdx.x < 64) {
+        const uint32_t g = threadIdx.x >> 3, cc = threadIdx.x & 7;
+        const int t = point_value(g, cc);
+        tbl.e[threadIdx.x] = (uint16_t)((t + 3) | ((sgn(t) + 1) << 4) | (possible_value(g) << 6));
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t b = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (b >= st.B) return;             // whole wave leaves together
+    const int cg = lane & 15;
+    const int y0 = (lane >> 4) * R;
+    const int64_t off = b * (int64_t)(H * 64);
+    Ctx c;
+    c.gb = reinterpret_cast<uint2 *>(st.board + off);
+    c.gg = reinterpret_cast<uint2 *>(st.goals + off);
+    c.gs = reinterpret_cast<const uint2 *>(st.start_board + off);
+    c.cg = cg;
+    c.y0 = y0;
+    c.gid = a.env0 + (uint32_t)b;
+    c.step = a.step;
+    c.seed = a.seed;
+
+    // -- rows needed before any store: halo above, first centre, halo below
+    const int ybot = wrap_row(y0 + R, H);
+    uint2 hb = c.gb[wrap_row(y0 - 1, H) * RW + cg], hg = c.gg[wrap_row(y0 - 1, H) * RW + cg];
+    uint2 vb = c.gb[y0 * RW + cg], vg = c.gg[y0 * RW + cg];
+    const uint2 tb2 = c.gb[ybot * RW + cg], tg2 = c.gg[ybot * RW + cg];
+    uint2 nxb[UNR], nxg[UNR];
+#pragma unroll
+    for (int j = 0; j < UNR; j++) {
+        if (1 + j < R) {
+            nxb[j] = c.gb[(y0 + 1 + j) * RW + cg];
+            nxg[j] = c.gg[(y0 + 1 + j) * RW + cg];
+        } else {
+            nxb[j] = tb2;
+            nxg[j] = tg2;
+        }
+    }
+
+    // -- the action, on lane 0 (its cell reads overlap the row loads above)
+    ActResult ar{0, 0, 0, 0};
+    Overlay ov;
+    ov.bd = st.board + off;
+    ov.n = 0;
+    if (lane == 0) ar = lane_action(st, b, actions[b], ctp, ctc, tbl, ov);
+    Edits ed;
+    ed.n = __builtin_amdgcn_readfirstlane(ov.n);
+    ed.rowmask = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        ed.y[k] = ed.cg[k] = ed.j[k] = ed.sh[k] = 0;
+        ed.v[k] = 0;
+        if (k < ed.n) {
+            const int i = __builtin_amdgcn_readfirstlane(ov.idx[k]);
+            const int ey = i >> 6, ex = i & 63;
+            ed.y[k] = ey;
+            ed.cg[k] = ex >> 2;
+            ed.j[k] = (ex >> 1) & 1;
+            ed.sh[k] = 16 * (ex & 1);
+            ed.v[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
+            const int r = ey % R;       // slot in its own strip, and the halo slots
+            ed.rowmask |= 1u << (r + 1);
+            if (r == R - 1) ed.rowmask |= 1u;          // halo above of the next strip
+            if (r == 0) ed.rowmask |= 1u << (R + 1);  // halo below of the previous strip
+        }
+    }
+    c.thr = (double)st.spawn_prob[b];
+
+    int d[4] = {0, 0, 0, 0};           // d points, d score, d possible, d side
+    if (st.spawn_flags[b])
+        strip_loop<H, UNR, true>(c, ed, tbl, hb, hg, vb, vg, tb2, tg2, nxb, nxg, d);
+    else
+        strip_loop<H, UNR, false>(c, ed, tbl, hb, hg, vb, vg, tb2, tg2, nxb, nxg, d);
 #pragma unroll
     for (int q = 0; q < 4; q++) d[q] = wave_sum(d[q]);
+    // every row store of this wave lands before lane 0 recolours the exit cells
+    __builtin_amdgcn_s_waitcnt(0);
     if (lane != 0) return;
-    const int64_t B = st.B;
-    const int points = st.old_points[b] + (int)act[B + b] + d[0];
-    const int score = st.score[b] + (int)act[2 * B + b] + d[1];
+    const int points = st.old_points[b] + ar.dp + d[0];
+    const int score = st.score[b] + ar.dq + d[1];
     const int possible = st.possible[b] + d[2];
-    const int side = st.side_effect[b] + (int)act[3 * B + b] + d[3];
-    env_epilogue(st, a, b, (int)act[b], points, score, possible, side, reward_out, done_out,
+    const int side = st.side_effect[b] + ar.dse + d[3];
+    env_epilogue(st, a, b, ar.reward, points, score, possible, side, reward_out, done_out,
                  flags_out, ep_len_out, ep_rew_out);
 }
 
@@ -332,22 +528,16 @@ k_env_step_w64(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
 
 namespace sl {
 
-bool launch_step_fast(const sl_env_state &st, const StepArgs &a, const int64_t *act,
-                      double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
-                      int32_t *ep_rew, hipStream_t s, int *rc) {
-    *rc = SL_OK;
-    if (st.W != 64) return false;
+bool fast_shape(int H, int W) { return W == 64 && H == 64; }
+
+int launch_step_fast(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
+                     int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
+                     int32_t *ep_rew, hipStream_t s) {
+    if (!fast_shape(st.H, st.W)) return SL_ETOOBIG;
     const unsigned grid = (unsigned)((st.B + 3) / 4);
-    switch (st.H) {
-        case 64:
-            hipLaunchKernelGGL((k_env_step_w64<64, SL_FAST_UNR>), dim3(grid), dim3(256), 0, s, st,
-                               a, act, reward, done, flags, ep_len, ep_rew);
-            break;
-        default:
-            return false;
-    }
-    if (hipGetLastError() != hipSuccess) *rc = SL_EHIP;
-    return true;
+    hipLaunchKernelGGL((k_env_step_w64<64, SL_FAST_UNR>), dim3(grid), dim3(256), 0, s, st, a,
+                       actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
 }  // namespace sl

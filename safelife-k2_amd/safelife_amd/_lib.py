@@ -40,7 +40,8 @@ class EnvState(ctypes.Structure):
                 ("side_effect", vp), ("spawn_prob", vp), ("min_performance", vp),
                 ("prior_x", vp), ("prior_y", vp), ("prior_len", vp), ("prior_head", vp),
                 ("exit_count", vp), ("exit_y", vp), ("exit_x", vp),
-                ("level_index", vp), ("episodes", vp), ("num_steps", vp)]
+                ("level_index", vp), ("episodes", vp), ("num_steps", vp),
+                ("spawn_flags", vp)]
 
 
 class LevelPool(ctypes.Structure):

@@ -113,7 +113,7 @@ class SafeLifeVecEnv:
             "prior_len": z(B), "prior_head": z(B), "exit_count": z(B),
             "exit_y": z(B, _lib.SL_MAX_EXITS, dt=torch.int16),
             "exit_x": z(B, _lib.SL_MAX_EXITS, dt=torch.int16),
-            "level_index": z(B), "episodes": z(B), "num_steps": z(B),
+            "level_index": z(B), "episodes": z(B), "num_steps": z(B), "spawn_flags": z(B),
         }
         s = _lib.EnvState()
         s.B, s.H, s.W = B, H, W
