@@ -45,6 +45,11 @@ constexpr uint32_t ONE2 = 0x00010001u;
 #ifndef SL_FAST_OCC
 #define SL_FAST_OCC 4      // waves per SIMD the register budget is sized for
 #endif
+// timing-only ablations (results are wrong when set): 1 no score deltas,
+// 2 no stores, 4 no rule (output = input)
+#ifndef SL_FAST_ABL
+#define SL_FAST_ABL 0
+#endif
 
 __device__ __forceinline__ uint32_t pk_shr(uint32_t val, uint32_t amt) {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -389,6 +394,10 @@ __device__ __forceinline__ void strip_loop(const Ctx &c, const Edits &ed, const 
                                         ngs.o0, ngs.t0, ngs.n0, &e2, &s2);
             uint32_t o3 = decide<SPAWN>(vg.y, wg1, pg.o1, pg.t1, pg.n1, cgs.o1, cgs.t1, cgs.n1,
                                         ngs.o1, ngs.t1, ngs.n1, &e3, &s3);
+            if (SL_FAST_ABL & 4) {
+                asm volatile("" :: "v"(o0), "v"(o1), "v"(o2), "v"(o3));
+                o0 = vb.x; o1 = vb.y; o2 = vg.x; o3 = vg.y;
+            }
             if (SPAWN) {
                 const bool any_e = (e0 | e1 | e2 | e3) != 0;
                 if (__ballot(any_e)) {
@@ -407,9 +416,11 @@ __device__ __forceinline__ void strip_loop(const Ctx &c, const Edits &ed, const 
             const bool sc_g = ((o2 ^ vg.x) | (o3 ^ vg.y)) != 0;
             const bool edited = ((ed.rowmask >> (r + 1)) & 1u) && has_edit(y, cg, ed);
             if (__ballot(sc_b || sc_g || edited)) {
-                if (sc_b || edited) c.gb[y * RW + cg] = make_uint2(o0, o1);
-                if (sc_g) c.gg[y * RW + cg] = make_uint2(o2, o3);
-                if (sc_b || sc_g)
+                if (!(SL_FAST_ABL & 2)) {
+                    if (sc_b || edited) c.gb[y * RW + cg] = make_uint2(o0, o1);
+                    if (sc_g) c.gg[y * RW + cg] = make_uint2(o2, o3);
+                }
+                if (!(SL_FAST_ABL & 1) && (sc_b || sc_g))
                     delta_row(tb, vb, make_uint2(o0, o1), vg, make_uint2(o2, o3),
                               c.gs[y * RW + cg], d);
             }

@@ -16,7 +16,7 @@ for r in range(rounds):
     for lib in libs:
         env = dict(os.environ, SAFELIFE_HIP_LIB=lib)
         out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "60",
-                              "--warmup", "10", "--no-cpu-baseline"] + extra,
+                              "--warmup", "10", "--no-cpu-baseline", "--burnin", "300"] + extra,
                              env=env, capture_output=True, text=True, timeout=300)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         if not line:
