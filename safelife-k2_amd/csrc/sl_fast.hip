@@ -50,6 +50,10 @@ constexpr uint32_t ONE2 = 0x00010001u;
 #ifndef SL_FAST_ABL
 #define SL_FAST_ABL 0
 #endif
+// 0: register-staged strips (4 envs per workgroup); 1: LDS-staged (1 env per workgroup)
+#ifndef SL_FAST_IMPL
+#define SL_FAST_IMPL 1
+#endif
 
 __device__ __forceinline__ uint32_t pk_shr(uint32_t val, uint32_t amt) {
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -161,9 +165,15 @@ struct ScoreTbl {
     uint16_t e[64];
 };
 
-__device__ __forceinline__ void cell_terms_lds(const ScoreTbl &tb, uint32_t b, uint32_t g,
+__device__ __forceinline__ uint32_t score_entry(uint32_t g, uint32_t c) {
+    const int t = point_value(g, c);
+    return (uint32_t)((t + 3) | ((sgn(t) + 1) << 4) | (possible_value(g) << 6));
+}
+
+__device__ __forceinline__ void cell_terms_lds(const ScoreTbl *tb, uint32_t b, uint32_t g,
                                                uint32_t s, int *p, int *q, int *r, int *se) {
-    const uint32_t e = tb.e[((g >> 6) & 0x38u) | ((b >> 9) & 7u)];
+    const uint32_t i = ((g >> 6) & 0x38u) | ((b >> 9) & 7u);
+    const uint32_t e = tb ? tb->e[i] : score_entry(i >> 3, i & 7);
     const bool alive = b & ALIVE;
     const bool m = alive && ((b & (FROZEN | MOVABLE)) != FROZEN);
     *p = alive ? (int)(e & 15u) - 3 : 0;
@@ -187,8 +197,8 @@ __device__ __forceinline__ void delta_row(const ScoreTbl &tb, uint2 ob, uint2 nb
             const uint32_t sv = (sw[j] >> sh) & 0xFFFF;
             if (o != n || go != gn) {
                 int p0, q0, r0, e0, p1, q1, r1, e1;
-                cell_terms_lds(tb, o, go, sv, &p0, &q0, &r0, &e0);
-                cell_terms_lds(tb, n, gn, sv, &p1, &q1, &r1, &e1);
+                cell_terms_lds(&tb, o, go, sv, &p0, &q0, &r0, &e0);
+                cell_terms_lds(&tb, n, gn, sv, &p1, &q1, &r1, &e1);
                 d[0] += p1 - p0;
                 d[1] += q1 - q0;
                 d[2] += r1 - r0;
@@ -233,7 +243,7 @@ __device__ __forceinline__ int pm(int a, int m) {
 }
 
 __device__ ActResult lane_action(const sl_env_state &st, int64_t b, int a, int ctp, int ctc,
-                                 const ScoreTbl &tb, Overlay &ov) {
+                                 const ScoreTbl *tb, Overlay &ov) {
     const int H = st.H, W = st.W;
     const int64_t hw = (int64_t)H * W;
     const uint16_t *gd = st.goals + b * hw, *sd = st.start_board + b * hw;
@@ -493,7 +503,7 @@ k_env_step_w64(sl_env_state st, StepArgs a, const int32_t *__restrict__ actions,
     Overlay ov;
     ov.bd = st.board + off;
     ov.n = 0;
-    if (lane == 0) ar = lane_action(st, b, actions[b], ctp, ctc, tbl, ov);
+    if (lane == 0) ar = lane_action(st, b, actions[b], ctp, ctc, &tbl, ov);
     Edits ed;
     ed.n = __builtin_amdgcn_readfirstlane(ov.n);
     ed.rowmask = 0;
@@ -535,6 +545,161 @@ k_env_step_w64(sl_env_state st, StepArgs a, const int32_t *__restrict__ actions,
                  flags_out, ep_len_out, ep_rew_out);
 }
 
+// ============================================================================
+// LDS-staged variant: one env per 128-thread workgroup (2 waves x 4 strips of
+// H/8 rows).  Each wave copies its half of the board and goals HBM -> LDS with
+// global_load_lds_dwordx4 (16 KiB per env in flight at once, no VGPRs), the
+// action is applied to the LDS copy and to memory by one lane, and the rows are
+// then read from LDS (wrapped halo rows included) by a rolled loop -- small
+// code, no register staging, every load of the env issued up front.
+// ============================================================================
+template <int H, int UNR, bool SPAWN>
+__device__ __forceinline__ void strip_loop_lds(const Ctx &c, const uint2 *lb, const uint2 *lg,
+                                               const ScoreTbl &tb, int R, int d[4]) {
+    constexpr int RW = 16;
+    const int cg = c.cg, y0 = c.y0;
+    uint2 hb = lb[wrap_row(y0 - 1, H) * RW + cg], hg = lg[wrap_row(y0 - 1, H) * RW + cg];
+    uint2 vb = lb[y0 * RW + cg], vg = lg[y0 * RW + cg];
+    CW wb0 = cword<SPAWN>(hb.x), wb1 = cword<SPAWN>(hb.y);
+    CW wg0 = cword<SPAWN>(hg.x), wg1 = cword<SPAWN>(hg.y);
+    RowSum pb = row_sum(wb0.c, wb1.c), pg = row_sum(wg0.c, wg1.c);
+    wb0 = cword<SPAWN>(vb.x); wb1 = cword<SPAWN>(vb.y);
+    wg0 = cword<SPAWN>(vg.x); wg1 = cword<SPAWN>(vg.y);
+    RowSum cb = row_sum(wb0.c, wb1.c), cgs = row_sum(wg0.c, wg1.c);
+#pragma unroll UNR
+    for (int r = 0; r < R; r++) {
+        const int y = y0 + r;                              // centre row
+        const int yn = wrap_row(y + 1, H);
+        const uint2 nb = lb[yn * RW + cg], ng = lg[yn * RW + cg];
+        const CW nb0w = cword<SPAWN>(nb.x), nb1w = cword<SPAWN>(nb.y);
+        const CW ng0w = cword<SPAWN>(ng.x), ng1w = cword<SPAWN>(ng.y);
+        const RowSum nbs = row_sum(nb0w.c, nb1w.c), ngs = row_sum(ng0w.c, ng1w.c);
+        uint32_t e0, e1, e2, e3, s0, s1, s2, s3;
+        uint32_t o0 = decide<SPAWN>(vb.x, wb0, pb.o0, pb.t0, pb.n0, cb.o0, cb.t0, cb.n0, nbs.o0,
+                                    nbs.t0, nbs.n0, &e0, &s0);
+        uint32_t o1 = decide<SPAWN>(vb.y, wb1, pb.o1, pb.t1, pb.n1, cb.o1, cb.t1, cb.n1, nbs.o1,
+                                    nbs.t1, nbs.n1, &e1, &s1);
+        uint32_t o2 = decide<SPAWN>(vg.x, wg0, pg.o0, pg.t0, pg.n0, cgs.o0, cgs.t0, cgs.n0,
+                                    ngs.o0, ngs.t0, ngs.n0, &e2, &s2);
+        uint32_t o3 = decide<SPAWN>(vg.y, wg1, pg.o1, pg.t1, pg.n1, cgs.o1, cgs.t1, cgs.n1,
+                                    ngs.o1, ngs.t1, ngs.n1, &e3, &s3);
+        if (SL_FAST_ABL & 4) {
+            asm volatile("" :: "v"(o0), "v"(o1), "v"(o2), "v"(o3));
+            o0 = vb.x; o1 = vb.y; o2 = vg.x; o3 = vg.y;
+        }
+        if (SPAWN) {
+            const bool any_e = (e0 | e1 | e2 | e3) != 0;
+            if (__ballot(any_e)) {
+                if (any_e) {
+                    const int cell = y * 64 + cg * 4;
+                    o0 = spawn_pair(o0, e0, s0, cell, c.gid, c.step, 0u, c.seed, c.thr);
+                    o1 = spawn_pair(o1, e1, s1, cell + 2, c.gid, c.step, 0u, c.seed, c.thr);
+                    o2 = spawn_pair(o2, e2, s2, cell, c.gid, c.step, 1u, c.seed, c.thr);
+                    o3 = spawn_pair(o3, e3, s3, cell + 2, c.gid, c.step, 1u, c.seed, c.thr);
+                }
+            }
+        }
+        const bool sc_b = ((o0 ^ vb.x) | (o1 ^ vb.y)) != 0;
+        const bool sc_g = ((o2 ^ vg.x) | (o3 ^ vg.y)) != 0;
+        if (__ballot(sc_b || sc_g)) {
+            if (!(SL_FAST_ABL & 2)) {
+                if (sc_b) c.gb[y * RW + cg] = make_uint2(o0, o1);
+                if (sc_g) c.gg[y * RW + cg] = make_uint2(o2, o3);
+            }
+            if (!(SL_FAST_ABL & 1) && (sc_b || sc_g))
+                delta_row(tb, vb, make_uint2(o0, o1), vg, make_uint2(o2, o3), c.gs[y * RW + cg],
+                          d);
+        }
+        pb = cb; cb = nbs; pg = cgs; cgs = ngs;
+        wb0 = nb0w; wb1 = nb1w; wg0 = ng0w; wg1 = ng1w;
+        vb = nb; vg = ng;
+    }
+}
+
+template <int H, int UNR>
+__global__ void __launch_bounds__(128)
+k_env_step_w64_lds(sl_env_state st, StepArgs a, const int32_t *__restrict__ actions, int ctp,
+                   int ctc, double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
+                   uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
+                   int32_t *__restrict__ ep_rew_out) {
+    constexpr int WPE = 2;                    // waves per env
+    constexpr int R = H / (4 * WPE);          // rows per strip
+    constexpr int HALF = H / WPE * 128;       // bytes of one wave's half board
+    __shared__ __attribute__((aligned(16))) uint2 lbd[H * 16];
+    __shared__ __attribute__((aligned(16))) uint2 lgd[H * 16];
+    __shared__ ScoreTbl tbl;
+    __shared__ int red[WPE][4];
+    const int64_t b = blockIdx.x;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t off = b * (int64_t)(H * 64);
+    {   // HBM -> LDS, this wave's half of board and goals, 1 KiB per instruction
+        const char *sb = reinterpret_cast<const char *>(st.board + off) + wv * HALF;
+        const char *sg = reinterpret_cast<const char *>(st.goals + off) + wv * HALF;
+        char *db = reinterpret_cast<char *>(lbd) + wv * HALF;
+        char *dg = reinterpret_cast<char *>(lgd) + wv * HALF;
+#pragma unroll
+        for (int k = 0; k < HALF / 1024; k++) {
+            __builtin_amdgcn_global_load_lds((const void *)(sb + k * 1024 + lane * 16),
+                                             (__attribute__((address_space(3))) void *)(db + k * 1024),
+                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *)(sg + k * 1024 + lane * 16),
+                                             (__attribute__((address_space(3))) void *)(dg + k * 1024),
+                                             16, 0, 0);
+        }
+    }
+    if (threadIdx.x < 64) {
+        const uint32_t g = threadIdx.x >> 3, cc = threadIdx.x & 7;
+        const int t = point_value(g, cc);
+        tbl.e[threadIdx.x] = (uint16_t)((t + 3) | ((sgn(t) + 1) << 4) | (possible_value(g) << 6));
+    }
+    // the action, on thread 0 (constant-memory score lookups: the LDS table is
+    // not ready before the barrier), while the copies are in flight
+    ActResult ar{0, 0, 0, 0};
+    Overlay ov;
+    ov.bd = st.board + off;
+    ov.n = 0;
+    if (threadIdx.x == 0) ar = lane_action(st, b, actions[b], ctp, ctc, nullptr, ov);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();                          // copies landed, table filled
+    if (threadIdx.x == 0) {
+        uint16_t *gbd = st.board + off;
+        uint16_t *lb16 = reinterpret_cast<uint16_t *>(lbd);
+        for (int k = 0; k < ov.n; k++) {
+            lb16[ov.idx[k]] = (uint16_t)ov.val[k];
+            gbd[ov.idx[k]] = (uint16_t)ov.val[k];
+        }
+    }
+    __syncthreads();                          // edits visible in LDS, stored in memory
+    Ctx c;
+    c.gb = reinterpret_cast<uint2 *>(st.board + off);
+    c.gg = reinterpret_cast<uint2 *>(st.goals + off);
+    c.gs = reinterpret_cast<const uint2 *>(st.start_board + off);
+    c.cg = lane & 15;
+    c.y0 = (wv * 4 + (lane >> 4)) * R;
+    c.gid = a.env0 + (uint32_t)b;
+    c.step = a.step;
+    c.seed = a.seed;
+    c.thr = (double)st.spawn_prob[b];
+    int d[4] = {0, 0, 0, 0};
+    if (st.spawn_flags[b])
+        strip_loop_lds<H, UNR, true>(c, lbd, lgd, tbl, R, d);
+    else
+        strip_loop_lds<H, UNR, false>(c, lbd, lgd, tbl, R, d);
+#pragma unroll
+    for (int q = 0; q < 4; q++) d[q] = wave_sum(d[q]);
+    if (lane == 0)
+        for (int q = 0; q < 4; q++) red[wv][q] = d[q];
+    __syncthreads();                          // every row store of both waves is done
+    if (threadIdx.x != 0) return;
+    for (int q = 0; q < 4; q++) d[q] = red[0][q] + red[1][q];
+    const int points = st.old_points[b] + ar.dp + d[0];
+    const int score = st.score[b] + ar.dq + d[1];
+    const int possible = st.possible[b] + d[2];
+    const int side = st.side_effect[b] + ar.dse + d[3];
+    env_epilogue(st, a, b, ar.reward, points, score, possible, side, reward_out, done_out,
+                 flags_out, ep_len_out, ep_rew_out);
+}
+
 }  // namespace
 
 namespace sl {
@@ -545,9 +710,14 @@ int launch_step_fast(const sl_env_state &st, const StepArgs &a, const int32_t *a
                      int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
                      int32_t *ep_rew, hipStream_t s) {
     if (!fast_shape(st.H, st.W)) return SL_ETOOBIG;
+#if SL_FAST_IMPL == 1
+    hipLaunchKernelGGL((k_env_step_w64_lds<64, SL_FAST_UNR>), dim3((unsigned)st.B), dim3(128), 0,
+                       s, st, a, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+#else
     const unsigned grid = (unsigned)((st.B + 3) / 4);
     hipLaunchKernelGGL((k_env_step_w64<64, SL_FAST_UNR>), dim3(grid), dim3(256), 0, s, st, a,
                        actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+#endif
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
