@@ -113,5 +113,9 @@ bool fast_shape(int H, int W);
 int launch_step_fast(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
                      int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
                      int32_t *ep_rew, hipStream_t s);
+// bit-sliced 64x64 kernel (sl_bits.hip)
+int launch_step_bits(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
+                     int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
+                     int32_t *ep_rew, hipStream_t s);
 
 }  // namespace sl

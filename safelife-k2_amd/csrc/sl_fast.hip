@@ -31,9 +31,12 @@
 //    LDS table lookup), the start-board read and the store are all skipped
 //    (wave-uniformly) on rows where nothing changed.  The totals equal the full
 //    sums the generic kernel computes (tests: test_fast_kernel_vs_generic).
-#include "sl_env_common.h"
+#include "sl_action.h"
+
+#pragma clang diagnostic ignored "-Wunneeded-internal-declaration"  // IMPL-specific helpers
 
 using namespace sl;
+using namespace sl::fast;
 
 namespace {
 
@@ -50,9 +53,10 @@ constexpr uint32_t ONE2 = 0x00010001u;
 #ifndef SL_FAST_ABL
 #define SL_FAST_ABL 0
 #endif
-// 0: register-staged strips (4 envs per workgroup); 1: LDS-staged (1 env per workgroup)
+// 0: register-staged strips (4 envs per workgroup); 1: LDS-staged (1 env per workgroup);
+// 2: bit-sliced columns (sl_bits.hip)
 #ifndef SL_FAST_IMPL
-#define SL_FAST_IMPL 1
+#define SL_FAST_IMPL 2
 #endif
 
 __device__ __forceinline__ uint32_t pk_shr(uint32_t val, uint32_t amt) {
@@ -158,30 +162,6 @@ __device__ __forceinline__ uint32_t spawn_pair(uint32_t o, uint32_t e, uint32_t 
     return o;
 }
 
-// ---------------------------------------------------------------- scoring
-// LDS lookup table, index (goal colour << 3) | cell colour:
-//   bits 0-3: point_table + 3, bits 4-5: sign(point_table) + 1, bit 6: max(sign row)
-struct ScoreTbl {
-    uint16_t e[64];
-};
-
-__device__ __forceinline__ uint32_t score_entry(uint32_t g, uint32_t c) {
-    const int t = point_value(g, c);
-    return (uint32_t)((t + 3) | ((sgn(t) + 1) << 4) | (possible_value(g) << 6));
-}
-
-__device__ __forceinline__ void cell_terms_lds(const ScoreTbl *tb, uint32_t b, uint32_t g,
-                                               uint32_t s, int *p, int *q, int *r, int *se) {
-    const uint32_t i = ((g >> 6) & 0x38u) | ((b >> 9) & 7u);
-    const uint32_t e = tb ? tb->e[i] : score_entry(i >> 3, i & 7);
-    const bool alive = b & ALIVE;
-    const bool m = alive && ((b & (FROZEN | MOVABLE)) != FROZEN);
-    *p = alive ? (int)(e & 15u) - 3 : 0;
-    *q = m ? (int)((e >> 4) & 3u) - 1 : 0;
-    *r = (int)((e >> 6) & 1u);
-    *se = side_term(b, s, g);
-}
-
 // score deltas of the 4 cells of a row that changed (board and/or goals)
 __device__ __forceinline__ void delta_row(const ScoreTbl &tb, uint2 ob, uint2 nb, uint2 og,
                                           uint2 ng, uint2 s, int d[4]) {
@@ -205,114 +185,6 @@ __device__ __forceinline__ void delta_row(const ScoreTbl &tb, uint2 ob, uint2 nb
                 d[3] += e1 - e0;
             }
         }
-}
-
-// ---------------------------------------------------------------- action
-// execute_action / move_agent (safelife_game.py:308-393) on a 4-cell overlay of
-// the board.  Run by one lane; produces the cell edits, the action reward and
-// the score deltas of the edited cells.
-struct Overlay {
-    int n;
-    int idx[4];
-    uint32_t val[4];
-    const uint16_t *bd;
-    __device__ uint32_t get(int i) const {
-        for (int k = 0; k < n; k++)
-            if (idx[k] == i) return val[k];
-        return bd[i];
-    }
-    __device__ void set(int i, uint32_t v) {
-        for (int k = 0; k < n; k++)
-            if (idx[k] == i) {
-                val[k] = v;
-                return;
-            }
-        idx[n] = i;
-        val[n] = v;
-        n++;
-    }
-};
-
-struct ActResult {
-    int reward, dp, dq, dse;
-};
-
-__device__ __forceinline__ int pm(int a, int m) {
-    int r = a % m;
-    return r < 0 ? r + m : r;
-}
-
-__device__ ActResult lane_action(const sl_env_state &st, int64_t b, int a, int ctp, int ctc,
-                                 const ScoreTbl *tb, Overlay &ov) {
-    const int H = st.H, W = st.W;
-    const int64_t hw = (int64_t)H * W;
-    const uint16_t *gd = st.goals + b * hw, *sd = st.start_board + b * hw;
-    ActResult res{0, 0, 0, 0};
-    ov.n = 0;
-    if (st.game_over[b] || a < 1 || a > 8) return res;
-    const int orient = (a - 1) & 3;
-    st.orientation[b] = orient;
-    const int fx = orient == 1 ? 1 : (orient == 3 ? -1 : 0);
-    const int fy = orient == 0 ? -1 : (orient == 2 ? 1 : 0);
-    const int x0 = st.agent_x[b], y0 = st.agent_y[b];
-    const int x1 = pm(x0 + fx, W), y1 = pm(y0 + fy, H);
-    const int i0 = y0 * W + x0, i1 = y1 * W + x1;
-    if (a <= 4) {
-        const int i2 = pm(y0 - fy, H) * W + pm(x0 - fx, W);
-        int nx = x0, ny = y0;
-        const uint32_t c1 = ov.get(i1);
-        if (c1 == 0) {
-            ov.set(i1, ov.get(i0));
-            ov.set(i0, 0);
-            nx = x1; ny = y1;
-        } else if ((c1 & EXIT) &&
-                   can_exit_now(st.min_performance[b], st.score[b], st.baseline[b],
-                                st.possible[b])) {
-            st.game_over[b] = 1;
-            res.reward = 1;
-        } else if (c1 & PUSHABLE) {
-            const int i3 = pm(y0 + 2 * fy, H) * W + pm(x0 + 2 * fx, W);
-            const uint32_t c3 = ov.get(i3);
-            if (c3 == 0) {
-                ov.set(i3, ov.get(i1));
-                ov.set(i1, ov.get(i0));
-                ov.set(i0, 0);
-                nx = x1; ny = y1;
-            } else if (c3 & EXIT) {
-                ov.set(i1, ov.get(i0));
-                ov.set(i0, 0);
-                nx = x1; ny = y1;
-            }
-        }
-        const bool moved = (nx == x1 && ny == y1) && !(x0 == x1 && y0 == y1);
-        if (moved && (ov.get(i2) & PULLABLE)) {
-            ov.set(i0, ov.get(i2));
-            ov.set(i2, 0);
-        }
-        st.agent_x[b] = nx;
-        st.agent_y[b] = ny;
-    } else {
-        const uint32_t pc = ov.get(i0) & COLORS;
-        const uint32_t t = ov.get(i1);
-        if (t == 0) {
-            ov.set(i1, LIFE | pc);
-        } else if (t & DESTR) {
-            ov.set(i1, 0);
-        } else {
-            const uint32_t tbits = (ctp ? POWERS : 0u) | (ctc ? COLORS : 0u);
-            ov.set(i0, ov.get(i0) ^ (t & tbits));
-        }
-    }
-    for (int k = 0; k < ov.n; k++) {
-        const int i = ov.idx[k];
-        int p0, q0, r0, e0, p1, q1, r1, e1;
-        cell_terms_lds(tb, ov.bd[i], gd[i], sd[i], &p0, &q0, &r0, &e0);
-        cell_terms_lds(tb, ov.val[k], gd[i], sd[i], &p1, &q1, &r1, &e1);
-        res.dp += p1 - p0;
-        res.dq += q1 - q0;
-        res.dse += e1 - e0;
-    }
-    return res;
 }
 
 __device__ __forceinline__ int wrap_row(int y, int H) { return y < 0 ? y + H : (y >= H ? y - H : y); }
@@ -710,7 +582,9 @@ int launch_step_fast(const sl_env_state &st, const StepArgs &a, const int32_t *a
                      int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
                      int32_t *ep_rew, hipStream_t s) {
     if (!fast_shape(st.H, st.W)) return SL_ETOOBIG;
-#if SL_FAST_IMPL == 1
+#if SL_FAST_IMPL == 2
+    return launch_step_bits(st, a, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew, s);
+#elif SL_FAST_IMPL == 1
     hipLaunchKernelGGL((k_env_step_w64_lds<64, SL_FAST_UNR>), dim3((unsigned)st.B), dim3(128), 0,
                        s, st, a, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
 #else

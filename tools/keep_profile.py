@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Copy a profile's judged artifacts from gpurun_out/ into profiles/ (tracked).
+
+Usage: keep_profile.py <gpurun_out/name> <tag> [--pmc-config c3]
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>_summary.json       per-kernel averages (all launches and timed window)
+  profiles/pmc_<config>.json        HBM bytes per launch of the step kernel (bench.py
+                                    reads it for roofline.traffic when the kernel matches)
+"""
+import glob
+import json
+import os
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(src, tag, cfg=None):
+    dst = os.path.join(REPO, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    st = glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True)[0]
+    shutil.copy(st, os.path.join(dst, tag + "_kernel_stats.csv"))
+    summ = json.load(open(os.path.join(src, "summary.json")))
+    json.dump(summ, open(os.path.join(dst, tag + "_summary.json"), "w"), indent=1, sort_keys=True)
+    if cfg:
+        step = [k for k in summ["kernels"] if "k_env_step" in k]
+        if len(step) != 1:
+            raise SystemExit("expected one step kernel, found %r" % step)
+        k = step[0]
+        d = summ["kernels"][k]
+        lk = d.get("last_k", {})
+        rec = {"kernel": k, "profile": tag,
+               "hbm_bytes_per_launch": lk.get("hbm_bytes_per_launch", d.get("hbm_bytes_per_launch")),
+               "hbm_read_bytes": lk.get("hbm_read_bytes", d.get("hbm_read_bytes")),
+               "hbm_write_bytes": lk.get("hbm_write_bytes", d.get("hbm_write_bytes")),
+               "avg_ns_timed_window": d.get("last_k_avg_ns"), "avg_ns_all": d.get("avg_ns"),
+               "note": "FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md HBM section), averaged "
+                       "over the bench's timed window (last %s launches)" % summ.get("last_k")}
+        json.dump(rec, open(os.path.join(dst, "pmc_%s.json" % cfg), "w"), indent=1)
+        print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    a = sys.argv[1:]
+    cfg = None
+    if "--pmc-config" in a:
+        i = a.index("--pmc-config")
+        cfg = a[i + 1]
+        del a[i:i + 2]
+    main(a[0], a[1], cfg)

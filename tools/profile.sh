@@ -1,14 +1,16 @@
 #!/bin/bash
-# Kernel trace + PMC passes for the headline bench (run on the GPU box).
-# Usage: tools/profile.sh <out_dir_name> [bench args...]
-# Writes gpurun_out/<name>/{kt,fetch,write,sq1,sq2}/ and a summary JSON.
+# Kernel trace + PMC passes over the headline bench command (run on the GPU box).
+# Usage: tools/profile.sh <out_dir_name> [extra bench args...]
+# Writes gpurun_out/<name>/{kt,fetch,write,sq1,sq2,tcc}/ and summary.json, whose
+# "last_k" fields average the bench's timed window (its last --steps launches).
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 NAME=${1:-prof}; shift || true
 OUT=$R/gpurun_out/$NAME
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 20 --warmup 4 --no-cpu-baseline $*"
+STEPS=200
+BENCH="$R/bench.py --steps $STEPS --warmup 20 --no-cpu-baseline $*"
 run() {  # name, rocprof args...
   local n=$1; shift
   timeout -k 10 400 rocprofv3 "$@" --output-format csv -d $OUT/$n -o $n -- python3 $BENCH > $OUT/$n.log 2>&1
@@ -19,6 +21,4 @@ run fetch --kernel-trace --pmc FETCH_SIZE || exit 1
 run write --kernel-trace --pmc WRITE_SIZE || exit 1
 run sq1 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES || exit 1
 run sq2 --kernel-trace --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE || exit 1
-run tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum || exit 1
-python3 $R/tools/pmc_summary.py $OUT > $OUT/summary.json
-cat $OUT/summary.json
+python3 $R/tools/pmc_summary.py $OUT --last $STEPS > $OUT/summary.json
