@@ -424,7 +424,7 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
     }
 }
 
-// grid-stride over envs: cheap when only a few envs reset this step
+// explicit resets (mask or all envs): grid-stride over envs, one block per env
 __global__ void __launch_bounds__(NT)
 k_env_reset(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ mask,
             const uint8_t *__restrict__ flags, ResetArgs a) {
@@ -433,6 +433,27 @@ k_env_reset(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ mas
         if (mask && !mask[b]) continue;
         if (flags && !(flags[b] & 4)) continue;
         reset_one(st, pool, a, b, sh);
+        __syncthreads();
+    }
+}
+
+// auto-reset after a step: each block checks NT envs' flags with one coalesced load,
+// gathers the finished ones (typically 0-2 of 256) and resets only those
+__global__ void __launch_bounds__(NT)
+k_env_reset_scan(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ flags,
+                 ResetArgs a) {
+    __shared__ ResetShared sh;
+    __shared__ int list[NT];
+    __shared__ int cnt;
+    const int64_t b0 = (int64_t)blockIdx.x * NT;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    const int64_t mine = b0 + threadIdx.x;
+    if (mine < st.B && (flags[mine] & 4)) list[atomicAdd(&cnt, 1)] = threadIdx.x;
+    __syncthreads();
+    const int n = cnt;
+    for (int k = 0; k < n; k++) {          // envs are independent: order is irrelevant
+        reset_one(st, pool, a, b0 + list[k], sh);
         __syncthreads();
     }
 }
@@ -632,9 +653,8 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     if (cfg->ev_end) (void)hipEventRecord((hipEvent_t)cfg->ev_end, s);
 
     if (cfg->auto_reset) {
-        hipLaunchKernelGGL(k_env_reset, dim3(reset_grid(B)), dim3(NT), 0, s, *st, *pool,
-                           (const uint8_t *)nullptr, (const uint8_t *)info_flags,
-                           reset_args(cfg));
+        hipLaunchKernelGGL(k_env_reset_scan, dim3((unsigned)((B + NT - 1) / NT)), dim3(NT), 0, s,
+                           *st, *pool, (const uint8_t *)info_flags, reset_args(cfg));
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
     }
     return SL_OK;

@@ -237,11 +237,16 @@ class SafeLifeVecEnv:
         a = torch.as_tensor(actions)
         if a.device != self.device or a.dtype != torch.int32:
             a = a.to(device=self.device, dtype=torch.int32)
-        self.actions_dev.copy_(a.reshape(self.B))
+        a = a.reshape(self.B)
+        if not a.is_contiguous():
+            a = a.contiguous()
+        # the kernel reads the caller's int32 device tensor in place (stream-ordered);
+        # keep a reference until the next step
+        self._actions_in_flight = a
         L = _lib.lib()
         cfg = self._fill_cfg()
         _lib.check(L.sl_env_step(ctypes.byref(self._state), ctypes.byref(self._pool_dev["struct"]),
-                                 self.actions_dev.data_ptr(), ctypes.byref(cfg),
+                                 a.data_ptr(), ctypes.byref(cfg),
                                  self.reward.data_ptr(), self.done.data_ptr(),
                                  self.flags.data_ptr(), self.ep_len.data_ptr(),
                                  self.ep_rew.data_ptr(), _lib.stream_ptr(self.device)),
