@@ -28,6 +28,8 @@
  *                       file_finder.py:143-201)
  *   sl_env_obs          SafeLifeEnv.get_obs (safelife_env.py:125-155) +
  *                       recenter_view (helper_utils.py:41-74)
+ *   sl_level_pool_prepare  derived pool data for the device level pool
+ *                       (levels as loaded by safelife_game.py:184-212)
  */
 #ifndef SAFELIFE_HIP_H
 #define SAFELIFE_HIP_H
@@ -46,7 +48,7 @@ extern "C" {
 #define SL_RNG_STREAM 0     /* replay a supplied uniform stream (reference order) */
 #define SL_RNG_PHILOX 1     /* counter-based Philox4x32-10 (production) */
 
-#define SL_KERNEL_AUTO 0     /* fast kernel when the shape has one (W == 64) */
+#define SL_KERNEL_AUTO 0     /* bit-sliced kernel for 64x64 in Philox mode */
 #define SL_KERNEL_GENERIC 1  /* LDS-staged per-cell kernel, any shape        */
 #define SL_KERNEL_FAST 2     /* require the fast kernel (error if none)      */
 
@@ -126,6 +128,11 @@ typedef struct sl_env_state {
     int32_t *spawn_flags;     /* bit0: board, bit1: goals hold a spawning cell
                                  (set at reset; spawning bits are never created
                                  by the rule or the actions, only moved)       */
+    int32_t *start_roll;      /* (dy << 16) | dx: start_board[b] equals pool
+                                 level level_index[b] rolled by (dy, dx) (set by
+                                 every reset); -1: start_board was written by
+                                 the caller.  Lets the 64x64 kernel read the
+                                 start board from the cache-resident pool.     */
 } sl_env_state;
 
 /* A device-resident level pool (the level_iterator's levels). */
@@ -137,7 +144,15 @@ typedef struct sl_level_pool {
     const float *spawn_prob;
     const double *min_performance;  /* the level's own value (used for the
                                        reset-time exit colour only)           */
+    uint64_t *board_planes;   /* [K,16,W] or NULL (64x64 pools): bit planes of
+                                 each board, element [k][p][x] has bit y = bit p
+                                 of board[k][y][x] (sl_level_pool_prepare)      */
 } sl_level_pool;
+
+/* Fill pool->board_planes (caller-allocated, dev uint64 [K,16,W]; H must be 64)
+ * from pool->board.  Derived data only; the reference keeps levels as npz
+ * (safelife_game.py:184-194). */
+int sl_level_pool_prepare(sl_level_pool *pool, void *stream);
 
 typedef struct sl_env_cfg {
     int32_t time_limit;             /* SafeLifeEnv.time_limit (1000)          */
@@ -176,7 +191,8 @@ typedef struct sl_env_cfg {
  *               bit2 env was reset this step
  *   ep_len, ep_reward  dev int32 [B] or NULL: finished-episode length / reward
  * With cfg->auto_reset the done/game-over envs are reset from `pool` before
- * returning (so the next sl_env_obs sees the new episode).
+ * returning (so the next sl_env_obs sees the new episode); the 64x64 kernel
+ * does this inside the step kernel, the other paths with a second kernel.
  */
 int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const int32_t *actions,
                 const sl_env_cfg *cfg, double *reward, uint8_t *done,

@@ -40,7 +40,8 @@ typedef uint32_t u32;
 #define SL_BITS_WPB 1        // envs (waves) per workgroup
 #endif
 #ifndef SL_BITS_MINW
-#define SL_BITS_MINW 3       // waves per SIMD the register budget is sized for
+#define SL_BITS_MINW 4       // waves per SIMD the register budget is sized for (the
+                             // rare reset path spills; the step path fits 128 VGPRs)
 #endif
 
 constexpr int N = 64;        // rows = columns = lanes
@@ -374,11 +375,150 @@ __device__ __forceinline__ void read_pairs(const lds_u32 *buf, int lane, u32 D[3
     for (int y = 0; y < 32; y++) D[y] = p[y * 32];
 }
 
+// The start-board planes the side-effect term needs (0, 2, 7-15), from the level
+// pool's precomputed bit planes: the start board of an env reset from the pool is
+// level li rolled by (dy, dx) (sl_env_state.start_roll).  Column c of the start
+// board is level column c - dx; its 64-bit row column rotated by dy gives rows
+// 32h .. 32h+31 as one funnel shift.  The pool stays in L2 / the Infinity Cache,
+// so this costs no HBM traffic and no transpose.
+__device__ __forceinline__ void pool_planes(const sl_level_pool &pool, int li, int dy, int dx,
+                                            int lane, u32 S[32]) {
+    const uint2 *pl = reinterpret_cast<const uint2 *>(pool.board_planes) + (int64_t)li * 16 * N;
+    const int c0 = (2 * (lane >> 1) - dx) & 63, c1 = (c0 + 1) & 63;
+    // bits 32h .. 32h+31 of rotl64(v, dy) = bits r .. r+31 of v, r = (32h - dy) mod 64
+    const int r = (32 * (lane & 1) - dy) & 63;
+    const bool lo_first = r < 32;
+    const u32 sh = (u32)(r & 31);
+#pragma unroll
+    for (int p = 0; p < 16; p++) {
+        if (p == 1 || (p >= 3 && p <= 6)) {        // player bits: not compared
+            PL(S, p, 0) = 0u;
+            PL(S, p, 1) = 0u;
+            continue;
+        }
+        const uint2 v0 = pl[p * N + c0], v1 = pl[p * N + c1];
+        PL(S, p, 0) = lo_first ? __builtin_amdgcn_alignbit(v0.y, v0.x, sh)
+                               : __builtin_amdgcn_alignbit(v0.x, v0.y, sh);
+        PL(S, p, 1) = lo_first ? __builtin_amdgcn_alignbit(v1.y, v1.x, sh)
+                               : __builtin_amdgcn_alignbit(v1.x, v1.y, sh);
+    }
+}
+
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs &a, int64_t b,
-                                         int lane, lds_u32 *buf,
+// SafeLifeEnv.reset (safelife_env.py:188-198) of env b by its own wave, right after
+// the step that finished the episode (ContinuingEnv + run_agents' reset-on-done).
+// Same result as reset_one (sl_env.hip): the rolled level is copied into board,
+// goals and start board; points, perf baseline and possible are the bit-sliced sums
+// over it; the exit list is collected row by row in np.nonzero order.
+__device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_level_pool &pool,
+                                        const ResetArgs &ra, int64_t b, int lane) {
+    int li = 0, dy = 0, dx = 0;
+    if (lane == 0) {
+        const LevelChoice c = choose_level(pool, ra, ra.env0 + (uint32_t)b, st.episodes[b], N, N);
+        li = c.idx;
+        dy = c.dy;
+        dx = c.dx;
+    }
+    li = __builtin_amdgcn_readfirstlane(li);
+    dy = __builtin_amdgcn_readfirstlane(dy);
+    dx = __builtin_amdgcn_readfirstlane(dx);
+    const int h = lane & 1, j = lane >> 1;
+    const uint16_t *lb = pool.board + (int64_t)li * (N * N), *lg = pool.goals + (int64_t)li * (N * N);
+    const int c0 = (2 * j - dx) & 63, c1 = (2 * j + 1 - dx) & 63;
+    const int64_t off = b * (int64_t)(N * N);
+    const int lane_off = h * 1024 + j;
+    u32 *gs = reinterpret_cast<u32 *>(st.start_board + off) + lane_off;
+    u32 *gg = reinterpret_cast<u32 *>(st.goals + off) + lane_off;
+    u32 *gb = reinterpret_cast<u32 *>(st.board + off) + lane_off;
+    // the lane's 32 dwords of a rolled pool level (8 rows of gathers in flight at a
+    // time: resets are rare, registers are not)
+    auto rolled = [&](const uint16_t *lv, u32 D[32]) {
+#pragma unroll
+        for (int y0 = 0; y0 < 32; y0 += 8) {
+#pragma unroll
+            for (int y = y0; y < y0 + 8; y++) {
+                const int sr = ((32 * h + y - dy) & 63) * N;
+                D[y] = (u32)lv[sr + c0] | ((u32)lv[sr + c1] << 16);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    // goals: copy, then keep their colour planes for the sums
+    u32 P[32];
+    rolled(lg, P);
+#pragma unroll
+    for (int y = 0; y < 32; y++) gg[y * 32] = P[y];
+    transpose32(P);
+    u32 gcol[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        gcol[k][0] = PL(P, 9 + k, 0);
+        gcol[k][1] = PL(P, 9 + k, 1);
+    }
+    const bool sg = __ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull;
+    __builtin_amdgcn_sched_barrier(0);
+    // start board: copy, then the sums over the initial board and goals
+    rolled(lb, P);
+#pragma unroll
+    for (int y = 0; y < 32; y++) gs[y * 32] = P[y];
+    transpose32(P);
+    int pts, scr, pos, side;
+    score_planes(P, gcol, P, &pts, &scr, &pos, &side);
+    const int s1 = wave_sum((pts + 192) | ((scr + 64) << 16));
+    const int s2 = wave_sum(pos);
+    const bool sb = __ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull;
+    int ev = 0;
+    if (lane == 0)
+        ev = reset_scalars(st, pool, ra, b, li, dy, dx, (s1 & 0xFFFF) - 192 * 64,
+                           ((s1 >> 16) & 0xFFFF) - 64 * 64, s2, (sb ? 1 : 0) | (sg ? 2 : 0));
+    ev = __builtin_amdgcn_readfirstlane(ev);
+    const u32 ex0 = PL(P, 8, 0), ex1 = PL(P, 8, 1);       // exit planes
+    __builtin_amdgcn_sched_barrier(0);
+    // the board: the start board with its exits coloured (update_exit_colors)
+    {
+        u32 D[32];
+        rolled(lb, D);
+#pragma unroll
+        for (int y = 0; y < 32; y++) {
+            u32 d = D[y];
+            if (d & (u32)EXIT) d = (d & 0xFFFF0000u) | (u32)ev;
+            if (d & ((u32)EXIT << 16)) d = (d & 0x0000FFFFu) | ((u32)ev << 16);
+            gb[y * 32] = d;
+        }
+    }
+    // exits in np.nonzero (row-major) order: per row, a column mask from two ballots
+    int n_exit = 0;
+    for (int r = 0; r < N; r++) {
+        const int y = r & 31, hr = r >> 5;
+        const bool mine = h == hr;
+        const uint64_t m0 = __ballot(mine && ((ex0 >> y) & 1u));
+        const uint64_t m1 = __ballot(mine && ((ex1 >> y) & 1u));
+        // column 2j <- bit 2j + hr of m0, column 2j + 1 <- bit 2j + hr of m1
+        const uint64_t ev_bits = 0x5555555555555555ull << hr;
+        uint64_t cm = ((m0 & ev_bits) >> hr) | (((m1 & ev_bits) >> hr) << 1);
+        while (cm) {
+            const int c = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            if (n_exit < SL_MAX_EXITS && lane == 0) {
+                st.exit_y[b * SL_MAX_EXITS + n_exit] = (int16_t)r;
+                st.exit_x[b * SL_MAX_EXITS + n_exit] = (int16_t)c;
+            }
+            n_exit++;
+        }
+    }
+    if (lane == 0) {
+        st.exit_count[b] = n_exit;
+        for (int e = n_exit; e < SL_MAX_EXITS; e++) {
+            st.exit_y[b * SL_MAX_EXITS + e] = 0;
+            st.exit_x[b * SL_MAX_EXITS + e] = 0;
+        }
+    }
+}
+
+__device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs &a,
+                                         const FastExtra &fx, int64_t b, int lane, lds_u32 *buf,
                                          const int32_t *__restrict__ actions, int ctp, int ctc,
                                          double *reward_out, uint8_t *done_out,
                                          uint8_t *flags_out, int32_t *ep_len_out,
@@ -435,12 +575,18 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     }
     __builtin_amdgcn_sched_barrier(0);
 
-    // ---- board: from LDS, then the start board takes over the buffer
+    // ---- board: from LDS; the start board comes from the level pool (cache) when
+    // the env was reset from it, else from HBM through the same LDS buffer
+    int roll = -1;
+    if (fx.pool.K > 0 && fx.pool.board_planes && st.start_roll) roll = st.start_roll[b];
+    roll = __builtin_amdgcn_readfirstlane(roll);
     wait_vm();
     u32 PB[32];
     read_pairs(buf, lane, PB);
-    wait_lgkm();
-    dma_board(st.start_board + off, buf, lane);
+    if (roll < 0) {
+        wait_lgkm();
+        dma_board(st.start_board + off, buf, lane);
+    }
     transpose32(PB);
     u32 erow = 0;                      // row pairs (y, y + 32) holding an edit
 #pragma unroll
@@ -465,10 +611,15 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- scores over the new board and goals
-    wait_vm();
     u32 PS[32];
-    read_pairs(buf, lane, PS);
-    transpose32(PS);
+    if (roll >= 0) {
+        pool_planes(fx.pool, __builtin_amdgcn_readfirstlane(st.level_index[b]), roll >> 16,
+                    roll & 0xFFFF, lane, PS);
+    } else {
+        wait_vm();
+        read_pairs(buf, lane, PS);
+        transpose32(PS);
+    }
     int pts, scr, pos, side;
     score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
     // totals (packed two per word: per-lane ranges [-192, 320] and [-64, 64]);
@@ -484,17 +635,23 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         store_pairs(gb, PB, rb);
     }
     __builtin_amdgcn_s_waitcnt(0);     // row stores done before lane 0 recolours exits
-    if (lane != 0) return;
-    const int points = (s1 & 0xFFFF) - 192 * 64;
-    const int score = ((s1 >> 16) & 0xFFFF) - 64 * 64;
-    const int possible = s2 & 0xFFFF;
-    const int side_total = (s2 >> 16) & 0xFFFF;
-    env_epilogue(st, a, b, act_reward, points, score, possible, side_total, reward_out, done_out,
-                 flags_out, ep_len_out, ep_rew_out);
+    int reset = 0;
+    if (lane == 0) {
+        const int points = (s1 & 0xFFFF) - 192 * 64;
+        const int score = ((s1 >> 16) & 0xFFFF) - 64 * 64;
+        const int possible = s2 & 0xFFFF;
+        const int side_total = (s2 >> 16) & 0xFFFF;
+        reset = env_epilogue(st, a, b, act_reward, points, score, possible, side_total,
+                             reward_out, done_out, flags_out, ep_len_out, ep_rew_out);
+    }
+    if (fx.fuse_reset && __builtin_amdgcn_readfirstlane(reset)) {
+        __builtin_amdgcn_s_waitcnt(0);     // the epilogue's exit stores land first
+        wave_reset(st, fx.pool, fx.ra, b, lane);
+    }
 }
 
 __global__ void __launch_bounds__(64 * SL_BITS_WPB, SL_BITS_MINW)
-k_env_step_bits64(sl_env_state st, StepArgs a, const int32_t *__restrict__ actions, int ctp,
+k_env_step_bits64(sl_env_state st, StepArgs a, FastExtra fx, const int32_t *__restrict__ actions, int ctp,
                   int ctc, double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
                   uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
                   int32_t *__restrict__ ep_rew_out) {
@@ -504,20 +661,20 @@ k_env_step_bits64(sl_env_state st, StepArgs a, const int32_t *__restrict__ actio
     __shared__ __attribute__((aligned(16))) u32 stage[SL_BITS_WPB][N * N / 2];
     if (b >= st.B) return;                 // whole waves only
     lds_u32 *buf = (lds_u32 *)&stage[threadIdx.x >> 6][0];
-    step_env(st, a, b, lane, buf, actions, ctp, ctc, reward_out, done_out, flags_out, ep_len_out,
-             ep_rew_out);
+    step_env(st, a, fx, b, lane, buf, actions, ctp, ctc, reward_out, done_out, flags_out,
+             ep_len_out, ep_rew_out);
 }
 
 }  // namespace
 
 namespace sl {
 
-int launch_step_bits(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
-                     int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
-                     int32_t *ep_rew, hipStream_t s) {
+int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
+                     const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
+                     uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (st.H != N || st.W != N) return SL_ETOOBIG;
     const unsigned grid = (unsigned)((st.B + SL_BITS_WPB - 1) / SL_BITS_WPB);
-    hipLaunchKernelGGL(k_env_step_bits64, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, st, a,
+    hipLaunchKernelGGL(k_env_step_bits64, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, st, a, fx,
                        actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }

@@ -303,15 +303,6 @@ k_env_step_generic(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
 // ---------------------------------------------------------------------------
 // reset from the level pool
 // ---------------------------------------------------------------------------
-struct ResetArgs {
-    int32_t toggle_powers;
-    double wrapper_min_perf;
-    uint64_t seed;
-    uint32_t env0;
-    int32_t level_mode, n_total, augment;
-    int32_t bonus_period;
-};
-
 struct ResetShared {
     int red[NT / 64][4];
     int wave_tot[NT / 64];
@@ -328,22 +319,8 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
     const int H = st.H, W = st.W, hw = H * W;
     const uint32_t gid = a.env0 + (uint32_t)b;
     if (threadIdx.x == 0) {
-        const int ep = st.episodes[b];
-        int idx;
-        if (a.level_mode == 1) {
-            idx = (int)(philox_uniform(gid, (uint32_t)ep, 0x5EEDu, 2u, a.seed) * pool.K);
-        } else {
-            idx = (int)(((int64_t)gid + (int64_t)ep * a.n_total) % pool.K);
-        }
-        idx = min(max(idx, 0), pool.K - 1);
-        int dy = 0, dx = 0;
-        if (a.augment) {
-            dy = (int)(philox_uniform(gid, (uint32_t)ep, 0x0011u, 3u, a.seed) * H);
-            dx = (int)(philox_uniform(gid, (uint32_t)ep, 0x0022u, 3u, a.seed) * W);
-            dy = min(dy, H - 1);
-            dx = min(dx, W - 1);
-        }
-        sh_idx = idx; sh_dy = dy; sh_dx = dx;
+        const LevelChoice c = choose_level(pool, a, gid, st.episodes[b], H, W);
+        sh_idx = c.idx; sh_dy = c.dy; sh_dx = c.dx;
     }
     __syncthreads();
     const int idx = sh_idx, dy = sh_dy, dx = sh_dx;
@@ -378,38 +355,13 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
     }
     block_sum4(acc, red);
     if (threadIdx.x == 0) {
-        const int points = acc[0], base = acc[1], possible = acc[2];
-        const double lvl_mp = pool.min_performance[idx];
-        const bool can = can_exit_now(lvl_mp, base, base, possible);
-        sh_ev = (int)(LEVEL_EXIT | (can ? COLOR_R : 0u));
-        const int ax = pymod(pool.agent_x[idx] + dx, W), ay = pymod(pool.agent_y[idx] + dy, H);
-        st.agent_x[b] = ax;
-        st.agent_y[b] = ay;
-        st.orientation[b] = pool.orientation[idx];
-        st.game_over[b] = 0;
-        st.num_steps[b] = 0;
-        st.spawn_flags[b] = ((acc[3] & 0xFFFF) || a.toggle_powers ? 1 : 0) |
-                            ((acc[3] >> 16) ? 2 : 0);
-        st.episode_length[b] = 0;
-        st.episode_reward[b] = 0;
-        st.old_points[b] = points;
-        st.baseline[b] = base;
-        st.score[b] = base;
-        st.possible[b] = possible;
-        st.side_effect[b] = 0;
-        st.spawn_prob[b] = pool.spawn_prob[idx];
-        st.min_performance[b] = isnan(a.wrapper_min_perf) ? lvl_mp : a.wrapper_min_perf;
+        const int spawn_bits = ((acc[3] & 0xFFFF) ? 1 : 0) | ((acc[3] >> 16) ? 2 : 0);
+        sh_ev = reset_scalars(st, pool, a, b, idx, dy, dx, acc[0], acc[1], acc[2], spawn_bits);
         st.exit_count[b] = n_exit;
         for (int e = 0; e < SL_MAX_EXITS; e++) {
             st.exit_y[b * SL_MAX_EXITS + e] = (int16_t)(e < n_exit ? sh_exit_y[e] : 0);
             st.exit_x[b * SL_MAX_EXITS + e] = (int16_t)(e < n_exit ? sh_exit_x[e] : 0);
         }
-        st.prior_x[b * SL_BONUS_PERIOD_MAX] = ax;
-        st.prior_y[b * SL_BONUS_PERIOD_MAX] = ay;
-        st.prior_len[b] = 1;
-        st.prior_head[b] = 0;
-        st.level_index[b] = idx;
-        st.episodes[b] = st.episodes[b] + 1;
     }
     __syncthreads();
     const uint16_t ev = (uint16_t)sh_ev;
@@ -421,6 +373,19 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
         gs[i] = vb;
         gb[i] = (vb & EXIT) ? ev : vb;
         gg[i] = pg[src];
+    }
+}
+
+// pool->board_planes[k][p][x] bit y = bit p of pool->board[k][y][x]  (H == 64)
+__global__ void __launch_bounds__(NT) k_pool_planes(sl_level_pool pool) {
+    const int64_t n = (int64_t)pool.K * 16 * pool.W;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+        const int64_t k = i / (16 * pool.W);
+        const int r = (int)(i - k * 16 * pool.W), p = r / pool.W, x = r - p * pool.W;
+        const uint16_t *bd = pool.board + k * 64 * pool.W + x;
+        uint64_t v = 0;
+        for (int y = 0; y < 64; y++) v |= (uint64_t)((bd[y * pool.W] >> p) & 1u) << y;
+        pool.board_planes[i] = v;
     }
 }
 
@@ -578,6 +543,16 @@ extern "C" int sl_event_elapsed_ms(void *begin, void *end, float *ms) {
                                                                                     : SL_EHIP;
 }
 
+extern "C" int sl_level_pool_prepare(sl_level_pool *pool, void *stream) {
+    if (!pool || pool->K <= 0 || pool->H != 64 || pool->W < 2 || !pool->board ||
+        !pool->board_planes)
+        return SL_EINVAL;
+    const int64_t n = (int64_t)pool->K * 16 * pool->W;
+    const unsigned grid = (unsigned)std::min<int64_t>((n + NT - 1) / NT, 4096);
+    hipLaunchKernelGGL(k_pool_planes, dim3(grid), dim3(NT), 0, (hipStream_t)stream, *pool);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
 extern "C" int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const uint8_t *mask,
                             const sl_env_cfg *cfg, void *stream) {
     if (!state_ok(st) || !pool || !cfg || pool->K <= 0 || pool->H != st->H || pool->W != st->W)
@@ -618,11 +593,19 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     const bool fast = cfg->rng_mode == SL_RNG_PHILOX && cfg->kernel != SL_KERNEL_GENERIC &&
                       fast_shape(st->H, st->W);
     if (cfg->kernel == SL_KERNEL_FAST && !fast) return SL_ETOOBIG;
+    bool reset_done = false;
     if (fast) {
+        FastExtra fx;
+        fx.fuse_reset = cfg->auto_reset ? 1 : 0;
+        if (pool) fx.pool = *pool;
+        else fx.pool = sl_level_pool{};
+        fx.ra = reset_args(cfg);
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
-        int rc = launch_step_fast(*st, a, actions, cfg->can_toggle_powers, cfg->can_toggle_colors,
-                                  reward, done, info_flags, ep_len, ep_reward, s);
+        int rc = launch_step_fast(*st, a, fx, actions, cfg->can_toggle_powers,
+                                  cfg->can_toggle_colors, reward, done, info_flags, ep_len,
+                                  ep_reward, s);
         if (rc) return rc;
+        reset_done = launch_fast_fuses_reset(*st, fx);
     } else {
         hipLaunchKernelGGL(k_env_action, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, *st,
                            actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act);
@@ -652,7 +635,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (cfg->ev_end) (void)hipEventRecord((hipEvent_t)cfg->ev_end, s);
 
-    if (cfg->auto_reset) {
+    if (cfg->auto_reset && !reset_done) {
         hipLaunchKernelGGL(k_env_reset_scan, dim3((unsigned)((B + NT - 1) / NT)), dim3(NT), 0, s,
                            *st, *pool, (const uint8_t *)info_flags, reset_args(cfg));
         if (hipGetLastError() != hipSuccess) return SL_EHIP;

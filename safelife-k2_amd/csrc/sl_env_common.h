@@ -45,7 +45,7 @@ __device__ __forceinline__ bool can_exit_now(double mp, int score, int baseline,
 // (safelife_game.py:531-537), MovementBonusWrapper.step (env_wrappers.py:67-88),
 // SimpleSideEffectPenalty.step (env_wrappers.py:319-346) and ContinuingEnv.step
 // (env_wrappers.py:298-303) in that order.
-__device__ __forceinline__ void env_epilogue(const sl_env_state &st, const StepArgs &a,
+__device__ __forceinline__ bool env_epilogue(const sl_env_state &st, const StepArgs &a,
                                              int64_t b, int act_reward, int points, int score,
                                              int possible, int side, double *reward_out,
                                              uint8_t *done_out, uint8_t *flags_out,
@@ -106,16 +106,97 @@ __device__ __forceinline__ void env_epilogue(const sl_env_state &st, const StepA
                                  ((a.auto_reset && completed) ? 4 : 0));
     if (ep_len_out) ep_len_out[b] = completed ? ep_len : 0;
     if (ep_rew_out) ep_rew_out[b] = completed ? ep_rew : 0;
+    return a.auto_reset && completed;      // the env is reset after this step
 }
 
-// fused fast path (sl_fast.hip): action + advance + scores in one kernel
+// ---------------------------------------------------------------------------
+// resets (SafeLifeEnv.reset, safelife_env.py:188-198, from a level pool)
+// ---------------------------------------------------------------------------
+struct ResetArgs {
+    int32_t toggle_powers;
+    double wrapper_min_perf;
+    uint64_t seed;
+    uint32_t env0;
+    int32_t level_mode, n_total, augment;
+    int32_t bonus_period;
+};
+
+struct LevelChoice {
+    int idx, dy, dx;
+};
+
+// the level and toroidal roll of env gid's episode `ep` (the level iterator's
+// choice, file_finder.py:143-201, made deterministic per global env id)
+__device__ __forceinline__ LevelChoice choose_level(const sl_level_pool &pool, const ResetArgs &a,
+                                                   uint32_t gid, int ep, int H, int W) {
+    int idx;
+    if (a.level_mode == 1)
+        idx = (int)(philox_uniform(gid, (uint32_t)ep, 0x5EEDu, 2u, a.seed) * pool.K);
+    else
+        idx = (int)(((int64_t)gid + (int64_t)ep * a.n_total) % pool.K);
+    idx = min(max(idx, 0), pool.K - 1);
+    int dy = 0, dx = 0;
+    if (a.augment) {
+        dy = min((int)(philox_uniform(gid, (uint32_t)ep, 0x0011u, 3u, a.seed) * H), H - 1);
+        dx = min((int)(philox_uniform(gid, (uint32_t)ep, 0x0022u, 3u, a.seed) * W), W - 1);
+    }
+    return LevelChoice{idx, dy, dx};
+}
+
+// Per-env scalar state of a fresh episode (SafeLifeEnv.reset + revert,
+// safelife_env.py:188-198, safelife_game.py:196-212; MovementBonusWrapper.reset and
+// SimpleSideEffectPenalty.reset, env_wrappers.py:90-94,313-317).  One thread.
+//   points / base / possible: sums over the (rolled) initial board and goals;
+//   spawn_bits: bit0 board, bit1 goals hold a spawning cell.  Returns the exit
+//   cell value the reset board carries (update_exit_colors after revert).
+__device__ __forceinline__ uint16_t reset_scalars(const sl_env_state &st,
+                                                  const sl_level_pool &pool, const ResetArgs &a,
+                                                  int64_t b, int idx, int dy, int dx, int points,
+                                                  int base, int possible, int spawn_bits) {
+    const int H = st.H, W = st.W;
+    const double lvl_mp = pool.min_performance[idx];
+    const bool can = can_exit_now(lvl_mp, base, base, possible);
+    const int ax = pymod(pool.agent_x[idx] + dx, W), ay = pymod(pool.agent_y[idx] + dy, H);
+    st.agent_x[b] = ax;
+    st.agent_y[b] = ay;
+    st.orientation[b] = pool.orientation[idx];
+    st.game_over[b] = 0;
+    st.num_steps[b] = 0;
+    st.spawn_flags[b] = ((spawn_bits & 1) || a.toggle_powers ? 1 : 0) | (spawn_bits & 2);
+    st.episode_length[b] = 0;
+    st.episode_reward[b] = 0;
+    st.old_points[b] = points;
+    st.baseline[b] = base;
+    st.score[b] = base;
+    st.possible[b] = possible;
+    st.side_effect[b] = 0;
+    st.spawn_prob[b] = pool.spawn_prob[idx];
+    st.min_performance[b] = isnan(a.wrapper_min_perf) ? lvl_mp : a.wrapper_min_perf;
+    st.prior_x[b * SL_BONUS_PERIOD_MAX] = ax;
+    st.prior_y[b * SL_BONUS_PERIOD_MAX] = ay;
+    st.prior_len[b] = 1;
+    st.prior_head[b] = 0;
+    st.level_index[b] = idx;
+    if (st.start_roll) st.start_roll[b] = (dy << 16) | dx;
+    st.episodes[b] = st.episodes[b] + 1;
+    return (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
+}
+
+// fused fast path (sl_fast.hip / sl_bits.hip): action + advance + scores (+ reset)
+struct FastExtra {
+    sl_level_pool pool;     // K == 0: no pool given
+    ResetArgs ra;
+    int32_t fuse_reset;     // auto-reset inside the step kernel
+};
 bool fast_shape(int H, int W);
-int launch_step_fast(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
-                     int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
-                     int32_t *ep_rew, hipStream_t s);
+int launch_step_fast(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
+                     const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
+                     uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
+// true when the launched fast kernel also performed the auto-resets
+bool launch_fast_fuses_reset(const sl_env_state &st, const FastExtra &fx);
 // bit-sliced 64x64 kernel (sl_bits.hip)
-int launch_step_bits(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
-                     int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
-                     int32_t *ep_rew, hipStream_t s);
+int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
+                     const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
+                     uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
 
 }  // namespace sl

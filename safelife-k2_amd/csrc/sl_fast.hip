@@ -578,16 +578,22 @@ namespace sl {
 
 bool fast_shape(int H, int W) { return W == 64 && H == 64; }
 
-int launch_step_fast(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
-                     int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
-                     int32_t *ep_rew, hipStream_t s) {
+bool launch_fast_fuses_reset(const sl_env_state &st, const FastExtra &fx) {
+    (void)st;
+    return SL_FAST_IMPL == 2 && fx.fuse_reset && fx.pool.K > 0;
+}
+
+int launch_step_fast(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
+                     const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
+                     uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (!fast_shape(st.H, st.W)) return SL_ETOOBIG;
 #if SL_FAST_IMPL == 2
-    return launch_step_bits(st, a, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew, s);
+    return launch_step_bits(st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew, s);
 #elif SL_FAST_IMPL == 1
     hipLaunchKernelGGL((k_env_step_w64_lds<64, SL_FAST_UNR>), dim3((unsigned)st.B), dim3(128), 0,
                        s, st, a, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
 #else
+    (void)fx;
     const unsigned grid = (unsigned)((st.B + 3) / 4);
     hipLaunchKernelGGL((k_env_step_w64<64, SL_FAST_UNR>), dim3(grid), dim3(256), 0, s, st, a,
                        actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);

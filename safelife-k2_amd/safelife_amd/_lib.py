@@ -41,13 +41,14 @@ class EnvState(ctypes.Structure):
                 ("prior_x", vp), ("prior_y", vp), ("prior_len", vp), ("prior_head", vp),
                 ("exit_count", vp), ("exit_y", vp), ("exit_x", vp),
                 ("level_index", vp), ("episodes", vp), ("num_steps", vp),
-                ("spawn_flags", vp)]
+                ("spawn_flags", vp), ("start_roll", vp)]
 
 
 class LevelPool(ctypes.Structure):
     _fields_ = [("K", i32), ("H", i32), ("W", i32),
                 ("board", vp), ("goals", vp), ("agent_x", vp), ("agent_y", vp),
-                ("orientation", vp), ("spawn_prob", vp), ("min_performance", vp)]
+                ("orientation", vp), ("spawn_prob", vp), ("min_performance", vp),
+                ("board_planes", vp)]
 
 
 class EnvCfg(ctypes.Structure):
@@ -94,13 +95,14 @@ def lib():
                               ctypes.POINTER(EnvCfg), vp, vp, vp, vp, vp, vp]
     L.sl_env_reset.argtypes = [ctypes.POINTER(EnvState), ctypes.POINTER(LevelPool), vp,
                                ctypes.POINTER(EnvCfg), vp]
+    L.sl_level_pool_prepare.argtypes = [ctypes.POINTER(LevelPool), vp]
     L.sl_env_obs.argtypes = [ctypes.POINTER(EnvState), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                              ctypes.c_int, vp, ctypes.c_int, vp, vp]
     L.sl_event_create.argtypes = [ctypes.POINTER(vp)]
     L.sl_event_destroy.argtypes = [vp]
     L.sl_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(f32)]
     for name in ("sl_event_create", "sl_event_destroy", "sl_event_elapsed_ms", "sl_device_arch", "sl_advance", "sl_count_eligible", "sl_exclusive_scan_i64",
-                 "sl_env_step", "sl_env_reset", "sl_env_obs"):
+                 "sl_env_step", "sl_env_reset", "sl_env_obs", "sl_level_pool_prepare"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

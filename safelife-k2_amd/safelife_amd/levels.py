@@ -8,6 +8,8 @@ shape lives on the GPU and the reset kernel copies level k (optionally with a
 random toroidal roll, under which the dynamics are exactly equivariant) into an
 env's board / goals / start board.
 """
+import ctypes
+
 import numpy as np
 
 from . import _lib
@@ -113,6 +115,14 @@ class LevelPool:
         for k in ("board", "goals", "agent_x", "agent_y", "orientation", "spawn_prob",
                   "min_performance"):
             setattr(s, k, t[k].data_ptr())
+        if self.H == 64:
+            # derived: per-level bit planes (the 64x64 kernel's start-board source)
+            t["board_planes"] = torch.empty((self.K, 16, self.W), dtype=torch.int64,
+                                            device=device)
+            s.board_planes = t["board_planes"].data_ptr()
+            L = _lib.lib()
+            _lib.check(L.sl_level_pool_prepare(ctypes.byref(s), _lib.stream_ptr(device)),
+                       "sl_level_pool_prepare")
         t["struct"] = s
         self._dev = t
         return t

@@ -114,6 +114,8 @@ class SafeLifeVecEnv:
             "exit_y": z(B, _lib.SL_MAX_EXITS, dt=torch.int16),
             "exit_x": z(B, _lib.SL_MAX_EXITS, dt=torch.int16),
             "level_index": z(B), "episodes": z(B), "num_steps": z(B), "spawn_flags": z(B),
+            # (dy << 16) | dx of the pool roll the start board came from; -1 = set by caller
+            "start_roll": z(B) - 1,
         }
         s = _lib.EnvState()
         s.B, s.H, s.W = B, H, W
@@ -277,6 +279,8 @@ class SafeLifeVecEnv:
         torch = self.torch
         for dst, src in ((self.board, board), (self.goals, goals), (self.start_board, start_board)):
             dst.copy_(torch.as_tensor(np.ascontiguousarray(src, dtype=np.uint16)).to(self.device))
+        # the start board no longer matches a pool level: kernels read it from HBM
+        self.st_t["start_roll"].fill_(-1)
         for k, v in scalars.items():
             t = self.st_t[k]
             t.copy_(torch.as_tensor(np.asarray(v)).to(device=self.device, dtype=t.dtype))
