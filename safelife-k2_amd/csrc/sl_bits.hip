@@ -26,7 +26,9 @@
 //    stored (a wave-wide OR of the per-column change masks picks them).
 // The action (execute_action / move_agent, safelife_game.py:308-393) runs on lane
 // 0 while the column loads are in flight; its cell edits are broadcast and
-// written into the planes before the rule.
+// written into the planes before the rule.  Envs that finish are queued; a second
+// kernel (k_env_reset_list) resets exactly those, one wave each, so the step
+// kernel carries no reset code (121 VGPRs, 4 waves/SIMD, no spills).
 #include "sl_action.h"
 
 using namespace sl;
@@ -40,8 +42,7 @@ typedef uint32_t u32;
 #define SL_BITS_WPB 1        // envs (waves) per workgroup
 #endif
 #ifndef SL_BITS_MINW
-#define SL_BITS_MINW 4       // waves per SIMD the register budget is sized for (the
-                             // rare reset path spills; the step path fits 128 VGPRs)
+#define SL_BITS_MINW 4       // waves per SIMD the register budget is sized for
 #endif
 
 constexpr int N = 64;        // rows = columns = lanes
@@ -121,10 +122,26 @@ __device__ __forceinline__ void load_pairs(const u32 *__restrict__ p, u32 D[32])
     for (int y = 0; y < 32; y++) D[y] = p[y * 32];
 }
 
+template <int CTRL>
+__device__ __forceinline__ u32 dpp(u32 v) {
+    return (u32)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int wave_total(int x) {
+    u32 v = (u32)x;
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return (int)((u32)__builtin_amdgcn_readlane((int)v, 0) + (u32)__builtin_amdgcn_readlane((int)v, 16) +
+                 (u32)__builtin_amdgcn_readlane((int)v, 32) + (u32)__builtin_amdgcn_readlane((int)v, 48));
+}
 __device__ __forceinline__ u32 wave_or(u32 v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v |= (u32)__shfl_xor((int)v, o, 64);
-    return (u32)__builtin_amdgcn_readfirstlane((int)v);
+    v |= dpp<0xB1>(v);
+    v |= dpp<0x4E>(v);
+    v |= dpp<0x141>(v);
+    v |= dpp<0x140>(v);
+    return (u32)__builtin_amdgcn_readlane((int)v, 0) | (u32)__builtin_amdgcn_readlane((int)v, 16) |
+           (u32)__builtin_amdgcn_readlane((int)v, 32) | (u32)__builtin_amdgcn_readlane((int)v, 48);
 }
 
 // ---------------------------------------------------------------- the rule
@@ -407,8 +424,8 @@ __device__ __forceinline__ void pool_planes(const sl_level_pool &pool, int li, i
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// SafeLifeEnv.reset (safelife_env.py:188-198) of env b by its own wave, right after
-// the step that finished the episode (ContinuingEnv + run_agents' reset-on-done).
+// SafeLifeEnv.reset (safelife_env.py:188-198) of env b by one wave, right after the
+// step that finished the episode (ContinuingEnv + run_agents' reset-on-done).
 // Same result as reset_one (sl_env.hip): the rolled level is copied into board,
 // goals and start board; points, perf baseline and possible are the bit-sliced sums
 // over it; the exit list is collected row by row in np.nonzero order.
@@ -466,8 +483,8 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
     transpose32(P);
     int pts, scr, pos, side;
     score_planes(P, gcol, P, &pts, &scr, &pos, &side);
-    const int s1 = wave_sum((pts + 192) | ((scr + 64) << 16));
-    const int s2 = wave_sum(pos);
+    const int s1 = wave_total((pts + 192) | ((scr + 64) << 16));
+    const int s2 = wave_total(pos);
     const bool sb = __ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull;
     int ev = 0;
     if (lane == 0)
@@ -624,8 +641,8 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
     // totals (packed two per word: per-lane ranges [-192, 320] and [-64, 64]);
     // reduced before the board store so the scoring is not sunk past it
-    const int s1 = wave_sum((pts + 192) | ((scr + 64) << 16));
-    const int s2 = wave_sum(pos | (side << 16));
+    const int s1 = wave_total((pts + 192) | ((scr + 64) << 16));
+    const int s2 = wave_total(pos | (side << 16));
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- write back the changed rows of the board
@@ -644,9 +661,11 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         reset = env_epilogue(st, a, b, act_reward, points, score, possible, side_total,
                              reward_out, done_out, flags_out, ep_len_out, ep_rew_out);
     }
-    if (fx.fuse_reset && __builtin_amdgcn_readfirstlane(reset)) {
-        __builtin_amdgcn_s_waitcnt(0);     // the epilogue's exit stores land first
-        wave_reset(st, fx.pool, fx.ra, b, lane);
+    if (fx.fuse_reset && reset && lane == 0) {
+        // queue the env for the reset kernel (k_env_reset_list)
+        int64_t *cnt = fx.scratch + 8 * st.B + 2 + (a.step & 1);
+        const int i = (int)atomicAdd((unsigned long long *)cnt, 1ull);
+        reinterpret_cast<int32_t *>(fx.scratch + 2 * st.B)[i] = (int32_t)b;
     }
 }
 
@@ -665,6 +684,19 @@ k_env_step_bits64(sl_env_state st, StepArgs a, FastExtra fx, const int32_t *__re
              ep_len_out, ep_rew_out);
 }
 
+// Resets the envs the step kernel queued (one wave per env, grid-stride over the
+// list).  Also zeroes the other step parity's list length for the next step.
+__global__ void __launch_bounds__(64)
+k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scratch,
+                 uint32_t step) {
+    int64_t *cnt = scratch + 8 * st.B + 2;
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(step + 1) & 1] = 0;
+    const int n = (int)__builtin_amdgcn_readfirstlane((int)cnt[step & 1]);
+    const int32_t *list = reinterpret_cast<const int32_t *>(scratch + 2 * st.B);
+    for (int i = blockIdx.x; i < n; i += gridDim.x)
+        wave_reset(st, pool, ra, __builtin_amdgcn_readfirstlane(list[i]), threadIdx.x);
+}
+
 }  // namespace
 
 namespace sl {
@@ -676,6 +708,12 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
     const unsigned grid = (unsigned)((st.B + SL_BITS_WPB - 1) / SL_BITS_WPB);
     hipLaunchKernelGGL(k_env_step_bits64, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, st, a, fx,
                        actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+    if (hipGetLastError() != hipSuccess) return SL_EHIP;
+    if (fx.fuse_reset && fx.pool.K > 0) {
+        const unsigned grid = (unsigned)(st.B < 8192 ? st.B : 8192);
+        hipLaunchKernelGGL(k_env_reset_list, dim3(grid), dim3(64), 0, s, st, fx.pool, fx.ra,
+                           fx.scratch, a.step);
+    }
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 

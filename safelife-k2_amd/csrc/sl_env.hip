@@ -600,6 +600,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         if (pool) fx.pool = *pool;
         else fx.pool = sl_level_pool{};
         fx.ra = reset_args(cfg);
+        fx.scratch = cfg->scratch;
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
         int rc = launch_step_fast(*st, a, fx, actions, cfg->can_toggle_powers,
                                   cfg->can_toggle_colors, reward, done, info_flags, ep_len,

@@ -7,10 +7,14 @@ namespace sl {
 
 // scratch layout (int64 words), see sl_env_cfg.scratch (8*B + 16 words):
 //   [0, 2B)   per-(env, tensor) draw counts      (replay mode)
-//   [2B, 4B)  per-(env, tensor) stream offsets   (replay mode)
+//   [2B, 4B)  per-(env, tensor) stream offsets   (replay mode); in Philox mode the
+//             first B int32 slots hold the list of envs to reset after the step
+//             (64x64 kernel)
 //   [4B, 8B)  per env: action reward, d_points, d_score, d_side of the action's
 //             cell edits (the fast path keeps the scores incrementally)
 //   [8B]      error flags (bit0: draw stream exhausted)
+//   [8B+2], [8B+3]  reset-list lengths for even / odd steps (each step's reset
+//             kernel zeroes the other one)
 struct Scratch {
     int64_t *counts, *offsets, *act, *err;
 };
@@ -39,7 +43,9 @@ __device__ __forceinline__ bool can_exit_now(double mp, int score, int baseline,
     return (double)(score - baseline) >= __dmul_rn(mp, (double)(possible - baseline));
 }
 
-// Per-env bookkeeping after the board advance, executed by one lane.
+// Per-env bookkeeping after the board advance.  Executed by one lane, or by a whole
+// wave with wave-uniform arguments (every lane then stores the same values, and the
+// integer work runs on the scalar unit).
 //   points / score / possible / side: the new totals over the advanced board.
 // Mirrors SafeLifeEnv.step (safelife_env.py:160-175), update_exit_colors
 // (safelife_game.py:531-537), MovementBonusWrapper.step (env_wrappers.py:67-88),
@@ -64,10 +70,8 @@ __device__ __forceinline__ bool env_epilogue(const sl_env_state &st, const StepA
     const bool can = can_exit_now(st.min_performance[b], score, st.baseline[b], possible);
     const uint16_t ev = (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
     const int ne = min(st.exit_count[b], SL_MAX_EXITS);
-    for (int e = 0; e < ne; e++) {
-        uint16_t *p = gb + st.exit_y[b * SL_MAX_EXITS + e] * W + st.exit_x[b * SL_MAX_EXITS + e];
-        if (*p != ev) *p = ev;
-    }
+    for (int e = 0; e < ne; e++)      // exits are frozen and never change otherwise
+        gb[st.exit_y[b * SL_MAX_EXITS + e] * W + st.exit_x[b * SL_MAX_EXITS + e]] = ev;
     const bool times_up = ep_len > a.time_limit;
     const bool over = st.game_over[b] != 0;
     const bool completed = times_up || over;
@@ -84,14 +88,14 @@ __device__ __forceinline__ bool env_epilogue(const sl_env_state &st, const StepA
         dist = min(dist, a.bonus_len - 1);
         r = __dadd_rn(r, a.bonus_table[dist]);
         if (len < n) {
-            const int slot = (head + len) % n;
+            const int slot = head + len >= n ? head + len - n : head + len;   // head, len < n
             px[slot] = ax;
             py[slot] = ay;
             st.prior_len[b] = len + 1;
         } else {
             px[head] = ax;
             py[head] = ay;
-            st.prior_head[b] = (head + 1) % n;
+            st.prior_head[b] = head + 1 == n ? 0 : head + 1;
         }
     }
     // reward -= delta_effect * coef: a rounded product, then a rounded difference
@@ -186,7 +190,9 @@ __device__ __forceinline__ uint16_t reset_scalars(const sl_env_state &st,
 struct FastExtra {
     sl_level_pool pool;     // K == 0: no pool given
     ResetArgs ra;
-    int32_t fuse_reset;     // auto-reset inside the step kernel
+    int32_t fuse_reset;     // auto-reset: the step kernel lists finished envs and a
+                            // follow-up kernel resets exactly those
+    int64_t *scratch;       // sl_env_cfg.scratch (reset list + counters)
 };
 bool fast_shape(int H, int W);
 int launch_step_fast(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
