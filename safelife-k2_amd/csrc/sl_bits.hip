@@ -449,17 +449,13 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
     u32 *gs = reinterpret_cast<u32 *>(st.start_board + off) + lane_off;
     u32 *gg = reinterpret_cast<u32 *>(st.goals + off) + lane_off;
     u32 *gb = reinterpret_cast<u32 *>(st.board + off) + lane_off;
-    // the lane's 32 dwords of a rolled pool level (8 rows of gathers in flight at a
-    // time: resets are rare, registers are not)
+    // the lane's 32 dwords of a rolled pool level (all gathers in flight at once:
+    // this runs in its own kernel, registers are plentiful)
     auto rolled = [&](const uint16_t *lv, u32 D[32]) {
 #pragma unroll
-        for (int y0 = 0; y0 < 32; y0 += 8) {
-#pragma unroll
-            for (int y = y0; y < y0 + 8; y++) {
-                const int sr = ((32 * h + y - dy) & 63) * N;
-                D[y] = (u32)lv[sr + c0] | ((u32)lv[sr + c1] << 16);
-            }
-            __builtin_amdgcn_sched_barrier(0);
+        for (int y = 0; y < 32; y++) {
+            const int sr = ((32 * h + y - dy) & 63) * N;
+            D[y] = (u32)lv[sr + c0] | ((u32)lv[sr + c1] << 16);
         }
     };
     // goals: copy, then keep their colour planes for the sums
@@ -475,7 +471,6 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
         gcol[k][1] = PL(P, 9 + k, 1);
     }
     const bool sg = __ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull;
-    __builtin_amdgcn_sched_barrier(0);
     // start board: copy, then the sums over the initial board and goals
     rolled(lb, P);
 #pragma unroll
@@ -492,7 +487,6 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
                            ((s1 >> 16) & 0xFFFF) - 64 * 64, s2, (sb ? 1 : 0) | (sg ? 2 : 0));
     ev = __builtin_amdgcn_readfirstlane(ev);
     const u32 ex0 = PL(P, 8, 0), ex1 = PL(P, 8, 1);       // exit planes
-    __builtin_amdgcn_sched_barrier(0);
     // the board: the start board with its exits coloured (update_exit_colors)
     {
         u32 D[32];
@@ -505,24 +499,30 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
             gb[y * 32] = d;
         }
     }
-    // exits in np.nonzero (row-major) order: per row, a column mask from two ballots
-    int n_exit = 0;
-    for (int r = 0; r < N; r++) {
-        const int y = r & 31, hr = r >> 5;
-        const bool mine = h == hr;
-        const uint64_t m0 = __ballot(mine && ((ex0 >> y) & 1u));
-        const uint64_t m1 = __ballot(mine && ((ex1 >> y) & 1u));
-        // column 2j <- bit 2j + hr of m0, column 2j + 1 <- bit 2j + hr of m1
-        const uint64_t ev_bits = 0x5555555555555555ull << hr;
-        uint64_t cm = ((m0 & ev_bits) >> hr) | (((m1 & ev_bits) >> hr) << 1);
-        while (cm) {
-            const int c = __builtin_ctzll(cm);
-            cm &= cm - 1;
-            if (n_exit < SL_MAX_EXITS && lane == 0) {
-                st.exit_y[b * SL_MAX_EXITS + n_exit] = (int16_t)r;
-                st.exit_x[b * SL_MAX_EXITS + n_exit] = (int16_t)c;
+    // exits in np.nonzero (row-major) order: repeatedly take the wave-wide smallest
+    // key row * 64 + column among the lanes' remaining exit bits (one round per exit)
+    const int n_exit = wave_total(__builtin_popcount(ex0) + __builtin_popcount(ex1));
+    {
+        u32 e0 = ex0, e1 = ex1;
+        const int kmax = n_exit < SL_MAX_EXITS ? n_exit : SL_MAX_EXITS;   // uniform
+        for (int k = 0; k < kmax; k++) {
+            const u32 k0 = e0 ? (u32)((32 * h + __builtin_ctz(e0)) * N + 2 * j) : 0xFFFFu;
+            const u32 k1 = e1 ? (u32)((32 * h + __builtin_ctz(e1)) * N + 2 * j + 1) : 0xFFFFu;
+            u32 m = k0 < k1 ? k0 : k1;
+            m = min(m, dpp<0xB1>(m));
+            m = min(m, dpp<0x4E>(m));
+            m = min(m, dpp<0x141>(m));
+            m = min(m, dpp<0x140>(m));
+            const u32 key = min(min((u32)__builtin_amdgcn_readlane((int)m, 0),
+                                    (u32)__builtin_amdgcn_readlane((int)m, 16)),
+                                min((u32)__builtin_amdgcn_readlane((int)m, 32),
+                                    (u32)__builtin_amdgcn_readlane((int)m, 48)));
+            if (k0 == key) e0 &= e0 - 1;
+            if (k1 == key) e1 &= e1 - 1;
+            if (lane == 0) {
+                st.exit_y[b * SL_MAX_EXITS + k] = (int16_t)(key >> 6);
+                st.exit_x[b * SL_MAX_EXITS + k] = (int16_t)(key & 63);
             }
-            n_exit++;
         }
     }
     if (lane == 0) {
@@ -710,7 +710,7 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
                        actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.fuse_reset && fx.pool.K > 0) {
-        const unsigned grid = (unsigned)(st.B < 8192 ? st.B : 8192);
+        const unsigned grid = (unsigned)(st.B < 512 ? st.B : 512);
         hipLaunchKernelGGL(k_env_reset_list, dim3(grid), dim3(64), 0, s, st, fx.pool, fx.ra,
                            fx.scratch, a.step);
     }
