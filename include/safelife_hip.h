@@ -133,6 +133,16 @@ typedef struct sl_env_state {
                                  every reset); -1: start_board was written by
                                  the caller.  Lets the 64x64 kernel read the
                                  start board from the cache-resident pool.     */
+    uint32_t *planes;         /* [B,2,32,64] or NULL (64x64 only): bit-plane
+                                 mirror of the goals (half 1; half 0 reserved)
+                                 kept by the 64x64 kernel: [b][1][q][lane],
+                                 word q = plane q & 15 of column 2(lane>>1) +
+                                 (q>>4), rows 32(lane&1)..+31 (sl_bits.hip).
+                                 Derived data, never read unless planes_ok
+                                 bit 1 is set.                                 */
+    int32_t *planes_ok;       /* [B] bit1: goals mirror valid.  Anything that
+                                 writes the goals other than the 64x64 kernel
+                                 and its reset clears it.                      */
 } sl_env_state;
 
 /* A device-resident level pool (the level_iterator's levels). */

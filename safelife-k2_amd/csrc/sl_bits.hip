@@ -41,6 +41,9 @@ typedef uint32_t u32;
 #ifndef SL_BITS_WPB
 #define SL_BITS_WPB 1        // envs (waves) per workgroup
 #endif
+#ifndef SL_BITS_MIRROR
+#define SL_BITS_MIRROR 1     // keep / use the bit-plane mirror of the goals
+#endif
 #ifndef SL_BITS_MINW
 #define SL_BITS_MINW 4       // waves per SIMD the register budget is sized for
 #endif
@@ -464,6 +467,11 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
 #pragma unroll
     for (int y = 0; y < 32; y++) gg[y * 32] = P[y];
     transpose32(P);
+    u32 *mg = (SL_BITS_MIRROR && st.planes) ? st.planes + b * 4096 + 2048 + lane : nullptr;
+    if (mg) {      // the goals' bit-plane mirror
+#pragma unroll
+        for (int q = 0; q < 32; q++) mg[q * 64] = P[q];
+    }
     u32 gcol[3][2];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -526,6 +534,7 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
         }
     }
     if (lane == 0) {
+        if (mg) st.planes_ok[b] = 2;   // after reset_scalars cleared it
         st.exit_count[b] = n_exit;
         for (int e = n_exit; e < SL_MAX_EXITS; e++) {
             st.exit_y[b * SL_MAX_EXITS + e] = 0;
@@ -544,9 +553,20 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     const int lane_off = (lane & 1) * 1024 + (lane >> 1);     // dwords: row 32h, column pair j
     u32 *gb = reinterpret_cast<u32 *>(st.board + off) + lane_off;
     u32 *gg = reinterpret_cast<u32 *>(st.goals + off) + lane_off;
-    dma_board(st.board + off, buf, lane);   // board -> LDS (no registers in flight)
+    // bit-plane mirrors (sl_env_state.planes): read instead of u16 + transpose when valid
+    // goals mirror, word-major: word q of lane l at planes[b*4096 + 2048 + q*64 + l]
+    // (the goals rarely change, so it saves their transpose at almost no write cost;
+    // a board mirror would be rewritten every step and does not pay)
+    u32 *mg = (SL_BITS_MIRROR && st.planes) ? st.planes + b * 4096 + 2048 + lane : nullptr;
+    const int pok = mg ? __builtin_amdgcn_readfirstlane(st.planes_ok[b]) & 2 : 0;
+    dma_board(st.board + off, buf, lane);                       // board cells -> LDS
     u32 PG[32];
-    load_pairs(gg, PG);                     // goals -> registers
+    if (pok & 2) {
+#pragma unroll
+        for (int q = 0; q < 32; q++) PG[q] = mg[q * 64];        // goal planes
+    } else {
+        load_pairs(gg, PG);                                     // goal cells
+    }
 
     // the action, on lane 0, while the loads are in flight
     Overlay ov;
@@ -576,9 +596,18 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     sc.thr = (double)st.spawn_prob[b];
 
     // ---- goals (independent of the action)
-    transpose32(PG);
+    if (!(pok & 2)) transpose32(PG);
     u32 cg[2];
     rule_planes(PG, cg, lane, sc, 1u);
+    if (mg) {      // mirror: the words whose 32 cells changed (all of them if rebuilt)
+        const bool all = !(pok & 2);
+#pragma unroll
+        for (int w = 0; w < 2; w++)
+            if (all || cg[w])
+#pragma unroll
+                for (int k = 0; k < 16; k++) mg[(k + 16 * w) * 64] = PL(PG, k, w);
+        if (!(pok & 2) && lane == 0) st.planes_ok[b] = 2;
+    }
     const u32 rg = wave_or(cg[0] | cg[1]);
     u32 gcol[3][2];                    // goal colour planes, kept for the scores
 #pragma unroll
@@ -645,22 +674,27 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     const int s2 = wave_total(pos | (side << 16));
     __builtin_amdgcn_sched_barrier(0);
 
-    // ---- write back the changed rows of the board
+    // ---- write back the changed rows of the board, exits already in the colour the
+    // epilogue gives them (update_exit_colors), so its exit writes and these row
+    // stores carry the same values and need no ordering
+    const int points = (s1 & 0xFFFF) - 192 * 64;
+    const int score = ((s1 >> 16) & 0xFFFF) - 64 * 64;
+    const int possible = s2 & 0xFFFF;
+    const int side_total = (s2 >> 16) & 0xFFFF;
     const u32 rb = wave_or(cb[0] | cb[1]) | erow;
     if (rb) {
+        const bool can = can_exit_now(st.min_performance[b], score, st.baseline[b], possible);
+#pragma unroll
+        for (int w = 0; w < 2; w++)
+            PL(PB, 9, w) = can ? (PL(PB, 9, w) | PL(PB, 8, w)) : (PL(PB, 9, w) & ~PL(PB, 8, w));
         transpose32(PB);
         store_pairs(gb, PB, rb);
     }
-    __builtin_amdgcn_s_waitcnt(0);     // row stores done before lane 0 recolours exits
     int reset = 0;
-    if (lane == 0) {
-        const int points = (s1 & 0xFFFF) - 192 * 64;
-        const int score = ((s1 >> 16) & 0xFFFF) - 64 * 64;
-        const int possible = s2 & 0xFFFF;
-        const int side_total = (s2 >> 16) & 0xFFFF;
+    if (lane == 0)
         reset = env_epilogue(st, a, b, act_reward, points, score, possible, side_total,
                              reward_out, done_out, flags_out, ep_len_out, ep_rew_out);
-    }
+    reset = __builtin_amdgcn_readfirstlane(reset);
     if (fx.fuse_reset && reset && lane == 0) {
         // queue the env for the reset kernel (k_env_reset_list)
         int64_t *cnt = fx.scratch + 8 * st.B + 2 + (a.step & 1);

@@ -55,6 +55,7 @@ k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int 
              int64_t *__restrict__ act) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= st.B) return;
+    if (st.planes_ok) st.planes_ok[b] = 0;    // this path does not keep the 64x64 mirror
     const int H = st.H, W = st.W;
     const int64_t hw = (int64_t)H * W;
     uint16_t *bd = st.board + b * hw;

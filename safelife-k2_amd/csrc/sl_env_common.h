@@ -182,6 +182,7 @@ __device__ __forceinline__ uint16_t reset_scalars(const sl_env_state &st,
     st.prior_head[b] = 0;
     st.level_index[b] = idx;
     if (st.start_roll) st.start_roll[b] = (dy << 16) | dx;
+    if (st.planes_ok) st.planes_ok[b] = 0;    // the 64x64 reset re-validates
     st.episodes[b] = st.episodes[b] + 1;
     return (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
 }

@@ -123,6 +123,12 @@ class SafeLifeVecEnv:
                                            self.start_board.data_ptr())
         for k, t in self.st_t.items():
             setattr(s, k, t.data_ptr())
+        # bit-plane mirror of board/goals kept by the 64x64 kernel (derived data)
+        self.planes_ok = z(B)
+        if (H, W) == (64, 64):
+            self.planes = z(B, 2, 32, 64)
+            s.planes = self.planes.data_ptr()
+            s.planes_ok = self.planes_ok.data_ptr()
         self._state = s
         self.actions_dev = z(B)
         self.reward = z(B, dt=torch.float64)
@@ -279,8 +285,10 @@ class SafeLifeVecEnv:
         torch = self.torch
         for dst, src in ((self.board, board), (self.goals, goals), (self.start_board, start_board)):
             dst.copy_(torch.as_tensor(np.ascontiguousarray(src, dtype=np.uint16)).to(self.device))
-        # the start board no longer matches a pool level: kernels read it from HBM
+        # the start board no longer matches a pool level: kernels read it from HBM;
+        # the bit-plane mirrors are stale
         self.st_t["start_roll"].fill_(-1)
+        self.planes_ok.zero_()
         for k, v in scalars.items():
             t = self.st_t[k]
             t.copy_(torch.as_tensor(np.asarray(v)).to(device=self.device, dtype=t.dtype))
@@ -293,6 +301,7 @@ class SafeLifeVecEnv:
         return d
 
     def load_state_dict(self, d):
+        self.planes_ok.zero_()             # mirrors are rebuilt by the next step
         self.board.copy_(d["board"])
         self.goals.copy_(d["goals"])
         self.start_board.copy_(d["start_board"])

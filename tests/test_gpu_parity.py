@@ -382,3 +382,38 @@ def test_full_batch_sampled_vs_oracle(torch_dev):
             assert np.array_equal(venv.goals[e].cpu().numpy(), oenvs[e].goals), ctx
     assert n_done > 0
     assert int(venv.state["episodes"].sum().item()) == B + n_done
+
+
+def test_fast_kernel_state_overwrite(torch_dev):
+    """set_state mid-run (board/goals/start written by the caller) invalidates the fast
+    kernel's bit-plane mirrors and pool start-board source: the run continues bit-exact
+    with the generic kernel given the same overwrite."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    path = os.path.join(GOLDEN, "pools", "c3_prune_still_64.npz")
+    B, T = 256, 60
+    kw = dict(time_limit=40, view_shape=(15, 15), output_channels=None, penalty_coef=1.0,
+              min_performance=0.01, rng="philox", seed=9, level_order="random",
+              augment_roll=True)
+    fast = SafeLifeVecEnv(LevelPool.load(path), B, "cuda:0", kernel="fast", **kw)
+    gen = SafeLifeVecEnv(LevelPool.load(path), B, "cuda:0", kernel="generic", **kw)
+    fast.reset()
+    gen.reset()
+    rng = np.random.RandomState(3)
+    for t in range(T):
+        a = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+        if t == 25:
+            # swap every env's state with its neighbour's (a state neither kernel's
+            # caches have seen), identically in both envs
+            perm = np.roll(np.arange(B), 1)
+            bd, gl, sb = (x.cpu().numpy()[perm] for x in (fast.board, fast.goals,
+                                                          fast.start_board))
+            sc = {k: v.cpu().numpy()[perm] for k, v in fast.st_t.items()
+                  if k != "start_roll"}
+            fast.set_state(bd, gl, sb, **sc)
+            gen.set_state(bd, gl, sb, **sc)
+        _, r1, d1, _ = fast.step(a)
+        _, r2, d2, _ = gen.step(a)
+        assert torch.equal(r1, r2), t
+        assert torch.equal(d1, d2), t
+        _compare_state(fast, gen, t)
