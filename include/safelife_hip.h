@@ -28,6 +28,8 @@
  *                       file_finder.py:143-201)
  *   sl_env_obs          SafeLifeEnv.get_obs (safelife_env.py:125-155) +
  *                       recenter_view (helper_utils.py:41-74)
+ *   sl_side_effect_densities  side_effect_score's rollout + density maps
+ *                       (side_effects.py:59-92,131-139), batched over episodes
  *   sl_level_pool_prepare  derived pool data for the device level pool
  *                       (levels as loaded by safelife_game.py:184-212)
  */
@@ -95,6 +97,41 @@ int sl_count_eligible(const uint16_t *in, int64_t *counts, int64_t B, int H, int
 /* out[i] = base + sum_{j<i} in[j]; *total_out (dev, may be NULL) = base + sum. */
 int sl_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n,
                           const int64_t *base, int64_t *total_out, void *stream);
+
+/* ------------------------------------------------------- side effects -- */
+
+/*
+ * The rollout + density half of side_effect_score (side_effects.py:59-92,
+ * 131-139) for E finished episodes at once.  Per episode e: b0 = init_board[e]
+ * is advanced num_steps[e] times, then num_samples times alternately with
+ * b1 = final_board[e] (b0 then b1, the reference's order); after each of those
+ * advances both boards are added to their cell-type density maps
+ * (_add_cell_distribution), which are finally divided by num_samples.
+ *   num_steps_dev / num_steps_host  the same [E] values, device and host copy
+ *   spawn_prob     dev float [E]
+ *   rng_mode       SL_RNG_STREAM: E must be 1; draws are consumed from
+ *                  draws[*stream_pos] on in the reference's order (advanced);
+ *                  SL_RNG_PHILOX: u = philox(seed; cell, env0 + e, advance
+ *                  index of that board, 4 + (0: b0, 1: b1)).
+ *   keys           dev uint16 [E, max_keys]: the union of both maps' cell-type
+ *                  keys, ascending; n_keys dev [E] its size (> max_keys means
+ *                  the maps are incomplete: raise max_keys); present dev
+ *                  [E, max_keys]: bit0 key occurs in the inaction map (b0),
+ *                  bit1 in the action map (b1)
+ *   inaction, action  dev double [E, max_keys, H, W] densities per key
+ *   workspace      dev scratch of sl_side_effect_workspace() bytes
+ * max_keys <= 1024.  The earth mover's distance over the maps
+ * (side_effects.py:12-56, third-party pyemd) is host code above this call.
+ */
+int sl_side_effect_workspace(int64_t E, int H, int W, int64_t *bytes);
+int sl_side_effect_densities(const uint16_t *init_board, const uint16_t *final_board,
+                             const int32_t *num_steps_dev, const int32_t *num_steps_host,
+                             const float *spawn_prob, int64_t E, int H, int W,
+                             int num_samples, int rng_mode, uint64_t seed, uint32_t env0,
+                             const double *draws, int64_t *stream_pos, int max_keys,
+                             uint16_t *keys, int32_t *n_keys, int32_t *present,
+                             double *inaction, double *action, void *workspace,
+                             int64_t workspace_bytes, void *stream);
 
 /* ------------------------------------------------------------------ envs -- */
 

@@ -188,6 +188,74 @@ def side_effect_count(board, start, goals, exit_mask):
     return int(np.sum(~non_effects))
 
 
+# --------------------------------------------------------------------------
+# side-effect rollout + densities (side_effects.py:59-92, 131-139)
+# --------------------------------------------------------------------------
+
+def density_key_board(board):
+    """Per-cell density key of _add_cell_distribution (side_effects.py:60-79):
+    0 = not counted; else the masked cell type (destructible restored for alive and
+    hard-spawner bases)."""
+    b = np.asarray(board, dtype=np.int64)
+    FROZEN_, DESTR_, MOVABLE_, AGENT_, COLORS_ = 0x10, 0x8, 0x4 | 0x8000, 0x2, 0xE00
+    unchanging = (b & (FROZEN_ | DESTR_ | MOVABLE_)) == FROZEN_       # side_effects.py:62
+    m = (b & ~DESTR_ & 0xFFFF) * ~unchanging                           # :63
+    skip = (m == 0) | ((m & AGENT_) != 0)                              # :69-71
+    base = m & ~COLORS_
+    key = np.where((base == 0x1) | (base == 0x90), m | DESTR_, m)      # :72-76
+    return np.where(skip, 0, key)
+
+
+def add_cell_distribution(board, dist):
+    """_add_cell_distribution (side_effects.py:59-86) on a {key: counts, 'n': n} dict."""
+    dist["n"] += 1
+    k = density_key_board(board)
+    for key in np.unique(k):
+        if key == 0:
+            continue
+        key = int(key)
+        if key not in dist:
+            dist[key] = np.zeros(k.shape)
+        dist[key] += k == key
+    return dist
+
+
+def norm_cell_distribution(dist):
+    """_norm_cell_distribution (side_effects.py:89-92)."""
+    n = dist.pop("n")
+    for x in dist.values():
+        x /= n
+
+
+def side_effect_densities(init_board, final_board, num_steps, spawn_prob, num_samples,
+                          rng="stream", stream=None, seed=0, env_id=0):
+    """The rollout of side_effect_score (side_effects.py:131-139): b0 from the initial
+    board advanced num_steps times, then num_samples x (b0, b1) advances, each pair
+    added to its density map.  rng 'stream' draws from stream.take() in the
+    reference's order; 'philox' keys a draw on (cell, env_id, advance index of that
+    board, 4 + board)."""
+    b0 = np.array(init_board, dtype=np.uint16)
+    b1 = np.array(final_board, dtype=np.uint16)
+    inaction, action = {"n": 0}, {"n": 0}
+
+    def adv(b, which, t):
+        if rng == "stream":
+            d = stream.take(count_eligible(b))
+            return advance(b, spawn_prob, d, 0, RNG_STREAM)[0]
+        return advance(b, spawn_prob, None, 0, RNG_PHILOX, seed, env_id, t, 4 + which)[0]
+
+    for t in range(num_steps):
+        b0 = adv(b0, 0, t)
+    for sidx in range(num_samples):
+        b0 = adv(b0, 0, num_steps + sidx)
+        b1 = adv(b1, 1, sidx)
+        add_cell_distribution(b0, inaction)
+        add_cell_distribution(b1, action)
+    norm_cell_distribution(inaction)
+    norm_cell_distribution(action)
+    return inaction, action
+
+
 def movement_bonus_table(n_max, bonus=0.1, power=0.01, period=4):
     """reward increment for each integer Manhattan distance (computed exactly as Python does)."""
     return np.array([bonus * (d / period) ** power for d in range(n_max + 1)],

@@ -96,13 +96,18 @@ def lib():
     L.sl_env_reset.argtypes = [ctypes.POINTER(EnvState), ctypes.POINTER(LevelPool), vp,
                                ctypes.POINTER(EnvCfg), vp]
     L.sl_level_pool_prepare.argtypes = [ctypes.POINTER(LevelPool), vp]
+    L.sl_side_effect_workspace.argtypes = [i64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64)]
+    L.sl_side_effect_densities.argtypes = [vp, vp, vp, vp, vp, i64, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, u64, u32, vp, vp,
+                                           ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, vp]
     L.sl_env_obs.argtypes = [ctypes.POINTER(EnvState), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                              ctypes.c_int, vp, ctypes.c_int, vp, vp]
     L.sl_event_create.argtypes = [ctypes.POINTER(vp)]
     L.sl_event_destroy.argtypes = [vp]
     L.sl_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(f32)]
     for name in ("sl_event_create", "sl_event_destroy", "sl_event_elapsed_ms", "sl_device_arch", "sl_advance", "sl_count_eligible", "sl_exclusive_scan_i64",
-                 "sl_env_step", "sl_env_reset", "sl_env_obs", "sl_level_pool_prepare"):
+                 "sl_env_step", "sl_env_reset", "sl_env_obs", "sl_level_pool_prepare",
+                 "sl_side_effect_workspace", "sl_side_effect_densities"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

@@ -417,3 +417,44 @@ def test_fast_kernel_state_overwrite(torch_dev):
         assert torch.equal(r1, r2), t
         assert torch.equal(d1, d2), t
         _compare_state(fast, gen, t)
+
+
+# ------------------------------------------------------- side-effect densities (A15)
+def test_side_effect_densities_reference_fixture(torch_dev):
+    """sl_side_effect_densities in replay mode reproduces the reference's density maps
+    (densities.npz, captured from side_effects.py with speedups.seed(11 + j))."""
+    from safelife_amd.side_effects import side_effect_densities
+    d = np.load(os.path.join(GOLDEN, "densities.npz"))
+    for j in range(2):
+        board = d["l%d_board" % j]
+        stream = np.random.RandomState(11 + j).random_sample(200000)
+        (ina, act), = side_effect_densities(board[None], np.roll(board, 1, axis=1)[None], [7],
+                                            float(d["l%d_spawn" % j]), 20, rng="stream",
+                                            spawn_stream=stream)
+        for nm, got in (("inaction", ina), ("action", act)):
+            keys = d["l%d_%s_keys" % (j, nm)].tolist()
+            assert sorted(got) == keys, (j, nm)
+            for k, ref in zip(keys, d["l%d_%s_dens" % (j, nm)]):
+                assert np.array_equal(got[k], ref), (j, nm, k)
+
+
+@pytest.mark.parametrize("pool_name", ["c2_append_still_25", "c3_prune_still_64"])
+def test_side_effect_densities_philox_batch_vs_oracle(torch_dev, pool_name):
+    """A batch of episodes with different num_steps (Philox) equals the oracle run of
+    each episode keyed by its index."""
+    from safelife_amd.side_effects import side_effect_densities
+    p = np.load(os.path.join(GOLDEN, "pools", pool_name + ".npz"))
+    E = 5
+    init = p["board"][:E]
+    rng = np.random.RandomState(4)
+    final = np.stack([np.roll(b, (rng.randint(3), rng.randint(3)), (0, 1)) for b in init])
+    steps = [0, 3, 11, 1, 6]
+    sp = 0.3
+    got = side_effect_densities(init, final, steps, sp, 9, rng="philox", seed=77, env0=0)
+    for e in range(E):
+        ina, act = oracle.side_effect_densities(init[e], final[e], steps[e], sp, 9,
+                                                rng="philox", seed=77, env_id=e)
+        for nm, g, r in (("inaction", got[e][0], ina), ("action", got[e][1], act)):
+            assert sorted(g) == sorted(r), (e, nm)
+            for k in r:
+                assert np.array_equal(g[k], r[k]), (e, nm, k)

@@ -124,3 +124,21 @@ def test_symmetry_deterministic():
             assert np.array_equal(t, out.T)
             f, _ = oracle.advance(np.ascontiguousarray(b[::-1]), p)
             assert np.array_equal(f, out[::-1])
+
+
+def test_g5_side_effect_densities():
+    """The oracle's rollout + density restatement reproduces the reference's
+    _add_cell_distribution maps captured in densities.npz (replay RNG)."""
+    d = np.load(os.path.join(GOLDEN, "densities.npz"))
+    for j in range(2):
+        stream = oracle.RefStreamRNG()
+        stream.seed(11 + j)
+        board = d["l%d_board" % j]
+        ina, act = oracle.side_effect_densities(board, np.roll(board, 1, axis=1), 7,
+                                                float(d["l%d_spawn" % j]), 20, rng="stream",
+                                                stream=stream)
+        for nm, got in (("inaction", ina), ("action", act)):
+            keys = d["l%d_%s_keys" % (j, nm)].tolist()
+            assert sorted(got) == keys, (j, nm)
+            for k, ref in zip(keys, d["l%d_%s_dens" % (j, nm)]):
+                assert np.array_equal(got[k], ref), (j, nm, k)
