@@ -46,6 +46,17 @@ class _RefBuffer:
         return np.concatenate(parts) if parts else np.zeros(0)
 
 
+    def peek(self, n):
+        """The next n draws without consuming them (numpy's global state and the
+        buffer are restored)."""
+        state, buf, pos = np.random.get_state(), self.buf, self.pos
+        try:
+            return self.take(n)
+        finally:
+            np.random.set_state(state)
+            self.buf, self.pos = buf, pos
+
+
 _buffer = _RefBuffer()
 
 

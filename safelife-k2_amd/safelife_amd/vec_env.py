@@ -154,6 +154,15 @@ class SafeLifeVecEnv:
         self._pool_dev = self.pool.to_device(self.device)
         self._cfg = _lib.EnvCfg()
 
+    def set_pool(self, levels):
+        """Replace the level pool the next resets draw from (same board shape)."""
+        pool = levels if isinstance(levels, LevelPool) else LevelPool.from_levels(levels)
+        if (pool.H, pool.W) != (self.H, self.W):
+            raise ValueError("pool boards are %dx%d, the env's %dx%d"
+                             % (pool.H, pool.W, self.H, self.W))
+        self.pool = pool
+        self._pool_dev = pool.to_device(self.device)
+
     def set_spawn_stream(self, stream, pos=0):
         """Uniform doubles consumed in reference order (rng='stream')."""
         torch = self.torch

@@ -72,3 +72,13 @@ def test_no_gpu_fails_loudly():
     import numpy as np
     with pytest.raises(_lib.HipUnavailable):
         speedups.advance_board(np.zeros((4, 4), np.uint16))
+    from safelife_amd import SafeLifeEnv, SafeLifeVecEnv, LevelPool
+    from safelife_amd.side_effects import side_effect_densities
+    level = {"board": np.zeros((8, 8), np.uint16), "goals": np.zeros((8, 8), np.uint16)}
+    with pytest.raises(_lib.HipUnavailable):
+        SafeLifeEnv(iter([level])).reset()
+    with pytest.raises(_lib.HipUnavailable):
+        SafeLifeVecEnv(LevelPool.from_levels([level]), 4)
+    with pytest.raises(_lib.HipUnavailable):
+        side_effect_densities(np.zeros((1, 8, 8), np.uint16), np.zeros((1, 8, 8), np.uint16),
+                              [0], 0.3, 2)

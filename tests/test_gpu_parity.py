@@ -458,3 +458,48 @@ def test_side_effect_densities_philox_batch_vs_oracle(torch_dev, pool_name):
             assert sorted(g) == sorted(r), (e, nm)
             for k in r:
                 assert np.array_equal(g[k], r[k]), (e, nm, k)
+
+
+# ------------------------------------------------------- B=1 drop-in views
+@pytest.mark.parametrize("path", _traj_files()[:6], ids=lambda p: os.path.basename(p)[5:-4])
+def test_single_env_dropin_golden(torch_dev, path):
+    """safelife_amd.SafeLifeEnv (B = 1, reference RNG through the global numpy stream)
+    reproduces a reference trajectory's boards, goals, agent state, points and
+    observations up to the first episode end (the wrappers only change the reward
+    and restart episodes), and leaves numpy's global RNG where the reference would."""
+    from safelife_amd import SafeLifeEnv
+    d = np.load(path)
+    penalty, min_perf, seed, vh, vw, time_limit = d["cfg"]
+    level = {"board": d["level_board"], "goals": d["level_goals"],
+             "agent_loc": d["level_agent_loc"], "orientation": d["level_orientation"],
+             "spawn_prob": d["level_spawn_prob"],
+             "min_performance": d["level_min_performance"]}
+    env = SafeLifeEnv(iter([level]), view_shape=(int(vh), int(vw)), output_channels=None,
+                      time_limit=int(time_limit), seed=int(seed))
+    obs0 = env.reset()
+    env.game.min_performance = float(min_perf)     # what SimpleSideEffectPenalty.reset does
+    assert np.array_equal(obs0, d["obs0"])
+    for t in range(len(d["action"])):
+        obs, r, done, info = env.step(int(d["action"][t]))
+        if d["done"][t] or d["game_over"][t] or d["episode_length"][t] == 0:
+            break
+        g = env.game
+        assert np.array_equal(g.board, d["board"][t]), t
+        assert np.array_equal(g.goals, d["goals"][t]), t
+        assert tuple(g.agent_loc) == tuple(d["agent_loc"][t]), t
+        assert g.orientation == d["orientation"][t], t
+        assert g.current_points() == d["points"][t], t
+        assert np.array_equal(obs, d["obs"][t]), t
+    # the global stream advanced exactly as the reference's draws did
+    ref = oracle.RefStreamRNG()
+    ref.seed(int(seed))
+    env2 = oracle.OracleEnv(lambda ep: oracle.Level(**{k: v for k, v in level.items()}),
+                            time_limit=int(time_limit), view_shape=(int(vh), int(vw)),
+                            output_channels=None, penalty_coef=0.0,
+                            min_performance=float(min_perf), rng="stream", stream=ref)
+    env2.reset()
+    for s in range(t + 1):
+        env2.step(int(d["action"][s]))
+    from safelife_amd import speedups
+    assert speedups._buffer.pos == ref.pos
+    assert np.array_equal(speedups._buffer.buf, ref.buf)
