@@ -41,6 +41,18 @@ typedef uint32_t u32;
 #ifndef SL_BITS_WPB
 #define SL_BITS_WPB 1        // envs (waves) per workgroup
 #endif
+#ifndef SL_BITS_UACT
+#define SL_BITS_UACT 0       // 1: the action runs wave-uniform (scalar unit); 0: on lane 0
+#endif
+#ifndef SL_BITS_UEPI
+#define SL_BITS_UEPI 0       // 1: the epilogue runs wave-uniform; 0: on lane 0
+#endif
+// timing-only ablations (results are wrong when set; never in the shipped build):
+//   1 no goals rule, 2 no board rule, 4 no scoring, 8 no board row stores,
+//   16 no action / epilogue
+#ifndef SL_BITS_ABL
+#define SL_BITS_ABL 0
+#endif
 #ifndef SL_BITS_MIRROR
 #define SL_BITS_MIRROR 1     // keep / use the bit-plane mirror of the goals
 #endif
@@ -578,7 +590,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         ov.val[k] = 0;
     }
     ActResult ar{0, 0, 0, 0};
-    if (lane == 0) ar = lane_action<false>(st, b, actions[b], ctp, ctc, nullptr, ov);
+    if (!(SL_BITS_ABL & 16) && (SL_BITS_UACT || lane == 0)) ar = lane_action<false>(st, b, actions[b], ctp, ctc, nullptr, ov);
     const int ne = __builtin_amdgcn_readfirstlane(ov.n);
     const int act_reward = __builtin_amdgcn_readfirstlane(ar.reward);
     int eidx[4];
@@ -598,7 +610,8 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     // ---- goals (independent of the action)
     if (!(pok & 2)) transpose32(PG);
     u32 cg[2];
-    rule_planes(PG, cg, lane, sc, 1u);
+    if (SL_BITS_ABL & 1) { cg[0] = cg[1] = 0; asm volatile("" : "+v"(PG[0])); }
+    else rule_planes(PG, cg, lane, sc, 1u);
     if (mg) {      // mirror: the words whose 32 cells changed (all of them if rebuilt)
         const bool all = !(pok & 2);
 #pragma unroll
@@ -653,7 +666,8 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         }
     }
     u32 cb[2];
-    rule_planes(PB, cb, lane, sc, 0u);
+    if (SL_BITS_ABL & 2) { cb[0] = PB[0] & 1; cb[1] = 0; }
+    else rule_planes(PB, cb, lane, sc, 0u);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- scores over the new board and goals
@@ -667,7 +681,8 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         transpose32(PS);
     }
     int pts, scr, pos, side;
-    score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
+    if (SL_BITS_ABL & 4) { pts = PB[3] & 3; scr = PS[5] & 1; pos = gcol[0][1] & 1; side = 0; }
+    else score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
     // totals (packed two per word: per-lane ranges [-192, 320] and [-64, 64]);
     // reduced before the board store so the scoring is not sunk past it
     const int s1 = wave_total((pts + 192) | ((scr + 64) << 16));
@@ -682,7 +697,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     const int possible = s2 & 0xFFFF;
     const int side_total = (s2 >> 16) & 0xFFFF;
     const u32 rb = wave_or(cb[0] | cb[1]) | erow;
-    if (rb) {
+    if (rb && !(SL_BITS_ABL & 8)) {
         const bool can = can_exit_now(st.min_performance[b], score, st.baseline[b], possible);
 #pragma unroll
         for (int w = 0; w < 2; w++)
@@ -691,7 +706,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         store_pairs(gb, PB, rb);
     }
     int reset = 0;
-    if (lane == 0)
+    if (!(SL_BITS_ABL & 16) && (SL_BITS_UEPI || lane == 0))
         reset = env_epilogue(st, a, b, act_reward, points, score, possible, side_total,
                              reward_out, done_out, flags_out, ep_len_out, ep_rew_out);
     reset = __builtin_amdgcn_readfirstlane(reset);
