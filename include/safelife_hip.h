@@ -177,9 +177,11 @@ typedef struct sl_env_state {
                                  (q>>4), rows 32(lane&1)..+31 (sl_bits.hip).
                                  Derived data, never read unless planes_ok
                                  bit 1 is set.                                 */
-    int32_t *planes_ok;       /* [B] bit1: goals mirror valid.  Anything that
-                                 writes the goals other than the 64x64 kernel
-                                 and its reset clears it.                      */
+    int32_t *planes_ok;       /* [B] bit1: goals mirror valid; bit2: goals at
+                                 a fixed point (no spawner, unchanged by the
+                                 last step: the rule is skipped).  Anything
+                                 that writes the goals other than the 64x64
+                                 kernel and its reset clears it.               */
 } sl_env_state;
 
 /* A device-resident level pool (the level_iterator's levels). */

@@ -32,13 +32,20 @@ __device__ __forceinline__ void cell_terms_lds(const ScoreTbl *tb, uint32_t b, u
 
 // ---------------------------------------------------------------- action
 // execute_action / move_agent (safelife_game.py:308-393) on a 4-cell overlay of
-// the board.  Run by one lane; produces the cell edits, the action reward and
-// the score deltas of the edited cells.
-struct Overlay {
+// the board.  Run by one lane (or wave-uniformly); produces the cell edits, the
+// action reward and (lane_action) the score deltas of the edited cells.
+//   Src: where the unedited cells come from (the board in HBM, or a copy in LDS)
+struct GlobalCells {
+    const uint16_t *bd;
+    __device__ __forceinline__ uint32_t operator()(int i) const { return bd[i]; }
+};
+
+template <class Src>
+struct OverlayT {
     int n;
     int idx[4];
     uint32_t val[4];
-    const uint16_t *bd;
+    Src src;
     // fully unrolled, statically indexed: the slots stay in registers
     __device__ uint32_t get(int i) const {
         uint32_t r = 0;
@@ -49,7 +56,7 @@ struct Overlay {
                 r = val[k];
                 hit = true;
             }
-        return hit ? r : (uint32_t)bd[i];
+        return hit ? r : src(i);
     }
     __device__ void set(int i, uint32_t v) {
         bool hit = false;
@@ -70,6 +77,7 @@ struct Overlay {
         }
     }
 };
+using Overlay = OverlayT<GlobalCells>;
 
 struct ActResult {
     int reward, dp, dq, dse;
@@ -80,20 +88,37 @@ __device__ __forceinline__ int pm(int a, int m) {
     return r < 0 ? r + m : r;
 }
 
-template <bool DELTA = true>
-__device__ ActResult lane_action(const sl_env_state &st, int64_t b, int a, int ctp, int ctc,
-                                 const ScoreTbl *tb, Overlay &ov) {
-    const int H = st.H, W = st.W;
-    const int64_t hw = (int64_t)H * W;
-    const uint16_t *gd = st.goals + b * hw, *sd = st.start_board + b * hw;
-    ActResult res{0, 0, 0, 0};
+// the per-env fields the action reads and writes, straight from sl_env_state
+struct GlobalEnv {
+    const sl_env_state &st;
+    int64_t b;
+    __device__ int game_over() const { return st.game_over[b]; }
+    __device__ int agent_x() const { return st.agent_x[b]; }
+    __device__ int agent_y() const { return st.agent_y[b]; }
+    __device__ bool can_exit() const {
+        return can_exit_now(st.min_performance[b], st.score[b], st.baseline[b], st.possible[b]);
+    }
+    __device__ void set_orientation(int o) { st.orientation[b] = o; }
+    __device__ void set_game_over() { st.game_over[b] = 1; }
+    __device__ void set_agent(int x, int y) {
+        st.agent_x[b] = x;
+        st.agent_y[b] = y;
+    }
+};
+
+// action a (0..8, safelife_env.py:61-71) on env e; the reward is 1 when the agent
+// walks into an open exit (move_agent, safelife_game.py:356-364), else 0
+template <class Env, class Src>
+__device__ __forceinline__ int act_core(Env &e, int a, int H, int W, int ctp, int ctc,
+                                        OverlayT<Src> &ov) {
     ov.n = 0;
-    if (st.game_over[b] || a < 1 || a > 8) return res;
+    if (e.game_over() || a < 1 || a > 8) return 0;
+    int reward = 0;
     const int orient = (a - 1) & 3;
-    st.orientation[b] = orient;
+    e.set_orientation(orient);
     const int fx = orient == 1 ? 1 : (orient == 3 ? -1 : 0);
     const int fy = orient == 0 ? -1 : (orient == 2 ? 1 : 0);
-    const int x0 = st.agent_x[b], y0 = st.agent_y[b];
+    const int x0 = e.agent_x(), y0 = e.agent_y();
     const int x1 = pm(x0 + fx, W), y1 = pm(y0 + fy, H);
     const int i0 = y0 * W + x0, i1 = y1 * W + x1;
     if (a <= 4) {
@@ -104,11 +129,9 @@ __device__ ActResult lane_action(const sl_env_state &st, int64_t b, int a, int c
             ov.set(i1, ov.get(i0));
             ov.set(i0, 0);
             nx = x1; ny = y1;
-        } else if ((c1 & EXIT) &&
-                   can_exit_now(st.min_performance[b], st.score[b], st.baseline[b],
-                                st.possible[b])) {
-            st.game_over[b] = 1;
-            res.reward = 1;
+        } else if ((c1 & EXIT) && e.can_exit()) {
+            e.set_game_over();
+            reward = 1;
         } else if (c1 & PUSHABLE) {
             const int i3 = pm(y0 + 2 * fy, H) * W + pm(x0 + 2 * fx, W);
             const uint32_t c3 = ov.get(i3);
@@ -128,8 +151,7 @@ __device__ ActResult lane_action(const sl_env_state &st, int64_t b, int a, int c
             ov.set(i0, ov.get(i2));
             ov.set(i2, 0);
         }
-        st.agent_x[b] = nx;
-        st.agent_y[b] = ny;
+        e.set_agent(nx, ny);
     } else {
         const uint32_t pc = ov.get(i0) & COLORS;
         const uint32_t t = ov.get(i1);
@@ -142,10 +164,21 @@ __device__ ActResult lane_action(const sl_env_state &st, int64_t b, int a, int c
             ov.set(i0, ov.get(i0) ^ (t & tbits));
         }
     }
+    return reward;
+}
+
+template <bool DELTA = true>
+__device__ ActResult lane_action(const sl_env_state &st, int64_t b, int a, int ctp, int ctc,
+                                 const ScoreTbl *tb, Overlay &ov) {
+    const int H = st.H, W = st.W;
+    const int64_t hw = (int64_t)H * W;
+    const uint16_t *gd = st.goals + b * hw, *sd = st.start_board + b * hw;
+    GlobalEnv e{st, b};
+    ActResult res{act_core(e, a, H, W, ctp, ctc, ov), 0, 0, 0};
     if (DELTA) for (int k = 0; k < ov.n; k++) {
         const int i = ov.idx[k];
         int p0, q0, r0, e0, p1, q1, r1, e1;
-        cell_terms_lds(tb, ov.bd[i], gd[i], sd[i], &p0, &q0, &r0, &e0);
+        cell_terms_lds(tb, ov.src(i), gd[i], sd[i], &p0, &q0, &r0, &e0);
         cell_terms_lds(tb, ov.val[k], gd[i], sd[i], &p1, &q1, &r1, &e1);
         res.dp += p1 - p0;
         res.dq += q1 - q0;

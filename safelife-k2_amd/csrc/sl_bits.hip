@@ -439,6 +439,131 @@ __device__ __forceinline__ void pool_planes(const sl_level_pool &pool, int li, i
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// ---------------------------------------------------------------- per-env record
+// The per-env fields the action, the spawn/start terms and the epilogue read are
+// fetched by ONE load instruction at kernel start: lane k of the record register
+// holds dword k below, and every later read is a v_readlane.  The lane-0 action and
+// epilogue then wait on no dependent HBM round trips (agent position -> cells,
+// ring head -> ring entry -> bonus); before, those chains cost ~27% of the kernel.
+enum : int {
+    R_ACT = 0, R_GO, R_AX, R_AY, R_SCORE, R_BASE, R_POSS, R_SPAWN, R_ROLL, R_LI, R_OLDP,
+    R_NSTEPS, R_EPLEN, R_EPREW, R_EXC, R_PLEN, R_PHEAD, R_SIDE, R_POK,
+    R_MP = 19,           // min_performance, 2 dwords
+    R_EY = 21,           // exit_y[8] (int16), 4 dwords
+    R_EX = 25,           // exit_x[8], 4 dwords
+    R_PX = 32,           // prior_x[16]
+    R_PY = 48            // prior_y[16]
+};
+
+__device__ __forceinline__ u32 load_record(const sl_env_state &st, const int32_t *actions,
+                                           int64_t b, int lane) {
+    const char *p = reinterpret_cast<const char *>(st.game_over);      // spare lanes
+    int64_t off = b * 4;
+#define SL_SEL(k, ptr)                                                                    \
+    if ((ptr) != nullptr) p = lane == (k) ? reinterpret_cast<const char *>(ptr) : p
+    SL_SEL(R_ACT, actions);
+    SL_SEL(R_AX, st.agent_x);
+    SL_SEL(R_AY, st.agent_y);
+    SL_SEL(R_SCORE, st.score);
+    SL_SEL(R_BASE, st.baseline);
+    SL_SEL(R_POSS, st.possible);
+    SL_SEL(R_SPAWN, st.spawn_prob);
+    SL_SEL(R_ROLL, st.start_roll);
+    SL_SEL(R_LI, st.level_index);
+    SL_SEL(R_OLDP, st.old_points);
+    SL_SEL(R_NSTEPS, st.num_steps);
+    SL_SEL(R_EPLEN, st.episode_length);
+    SL_SEL(R_EPREW, st.episode_reward);
+    SL_SEL(R_EXC, st.exit_count);
+    SL_SEL(R_PLEN, st.prior_len);
+    SL_SEL(R_PHEAD, st.prior_head);
+    SL_SEL(R_SIDE, st.side_effect);
+    SL_SEL(R_POK, st.planes_ok);
+#undef SL_SEL
+    if (lane >= R_MP && lane < R_MP + 2) {
+        p = reinterpret_cast<const char *>(st.min_performance);
+        off = b * 8 + 4 * (lane - R_MP);
+    } else if (lane >= R_EY && lane < R_EY + 4) {
+        p = reinterpret_cast<const char *>(st.exit_y);
+        off = b * 16 + 4 * (lane - R_EY);
+    } else if (lane >= R_EX && lane < R_EX + 4) {
+        p = reinterpret_cast<const char *>(st.exit_x);
+        off = b * 16 + 4 * (lane - R_EX);
+    } else if (lane >= R_PX) {
+        p = reinterpret_cast<const char *>(lane < R_PY ? st.prior_x : st.prior_y);
+        off = b * 64 + 4 * ((lane - R_PX) & 15);
+    }
+    return *reinterpret_cast<const u32 *>(p + off);
+}
+
+__device__ __forceinline__ int rec(u32 V, int k) { return __builtin_amdgcn_readlane((int)V, k); }
+__device__ __forceinline__ double rec_f64(u32 V, int k) {
+    return __hiloint2double(rec(V, k + 1), rec(V, k));
+}
+
+// the action's view of the env: record fields in, state writes out
+struct RecEnv {
+    const sl_env_state &st;
+    int64_t b;
+    int go, ax, ay, score, base, poss;
+    double mp;
+    __device__ int game_over() const { return go; }
+    __device__ int agent_x() const { return ax; }
+    __device__ int agent_y() const { return ay; }
+    __device__ bool can_exit() const { return can_exit_now(mp, score, base, poss); }
+    __device__ void set_orientation(int o) { st.orientation[b] = o; }
+    __device__ void set_game_over() {
+        go = 1;
+        st.game_over[b] = 1;
+    }
+    __device__ void set_agent(int x, int y) {
+        ax = x;
+        ay = y;
+        st.agent_x[b] = x;
+        st.agent_y[b] = y;
+    }
+};
+
+// the epilogue's view (epilogue_core): record fields plus the post-action agent
+struct RecFields {
+    u32 V;
+    int go, ax, ay;
+    double bval;
+    __device__ int old_points() const { return rec(V, R_OLDP); }
+    __device__ int num_steps() const { return rec(V, R_NSTEPS); }
+    __device__ int episode_length() const { return rec(V, R_EPLEN); }
+    __device__ int episode_reward() const { return rec(V, R_EPREW); }
+    __device__ double min_performance() const { return rec_f64(V, R_MP); }
+    __device__ int baseline() const { return rec(V, R_BASE); }
+    __device__ int exit_count() const { return rec(V, R_EXC); }
+    __device__ int exit_y(int e) const {
+        return (int)(int16_t)(rec(V, R_EY + (e >> 1)) >> (16 * (e & 1)));
+    }
+    __device__ int exit_x(int e) const {
+        return (int)(int16_t)(rec(V, R_EX + (e >> 1)) >> (16 * (e & 1)));
+    }
+    __device__ int game_over() const { return go; }
+    __device__ int agent_x() const { return ax; }
+    __device__ int agent_y() const { return ay; }
+    __device__ int prior_len() const { return rec(V, R_PLEN); }
+    __device__ int prior_head() const { return rec(V, R_PHEAD); }
+    __device__ int prior_x(int k) const { return rec(V, R_PX + k); }
+    __device__ int prior_y(int k) const { return rec(V, R_PY + k); }
+    __device__ int side_effect() const { return rec(V, R_SIDE); }
+    __device__ double bonus(int) const { return bval; }
+};
+
+// unedited cells for the action, from the staged board (dma_board's layout)
+typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+struct LdsCells {
+    const lds_u32 *buf;
+    __device__ __forceinline__ uint32_t operator()(int i) const {
+        const int row = i >> 6, col = i & 63;
+        const int pos = ((col >> 3) + ((row >> 5) << 2)) & 7;
+        return reinterpret_cast<lds_cu16 *>(buf)[row * 64 + pos * 8 + (col & 7)];
+    }
+};
+
 // SafeLifeEnv.reset (safelife_env.py:188-198) of env b by one wave, right after the
 // step that finished the episode (ContinuingEnv + run_agents' reset-on-done).
 // Same result as reset_one (sl_env.hip): the rolled level is copied into board,
@@ -570,29 +695,87 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     // (the goals rarely change, so it saves their transpose at almost no write cost;
     // a board mirror would be rewritten every step and does not pay)
     u32 *mg = (SL_BITS_MIRROR && st.planes) ? st.planes + b * 4096 + 2048 + lane : nullptr;
-    const int pok = mg ? __builtin_amdgcn_readfirstlane(st.planes_ok[b]) & 2 : 0;
+    const u32 V = load_record(st, actions, b, lane);           // issued first
     dma_board(st.board + off, buf, lane);                       // board cells -> LDS
-    u32 PG[32];
-    if (pok & 2) {
+    // goals: a goals board without spawners that came through a step unchanged is at
+    // a fixed point of the (then deterministic) rule and never changes again
+    // (planes_ok bit 2); such envs read only the three colour planes of the mirror,
+    // which are speculatively in flight before the record says which case holds
+    u32 gcol[3][2];                    // goal colour planes, kept for the scores
+    if (mg) {
 #pragma unroll
-        for (int q = 0; q < 32; q++) PG[q] = mg[q * 64];        // goal planes
-    } else {
-        load_pairs(gg, PG);                                     // goal cells
+        for (int k = 0; k < 3; k++) {
+            gcol[k][0] = mg[(9 + k) * 64];
+            gcol[k][1] = mg[(25 + k) * 64];
+        }
     }
+    const int pok = (mg && st.planes_ok) ? rec(V, R_POK) & 6 : 0;
 
-    // the action, on lane 0, while the loads are in flight
-    Overlay ov;
-    ov.bd = st.board + off;
+    SpawnCtx sc;
+    sc.gid = a.env0 + (uint32_t)b;
+    sc.step = a.step;
+    sc.seed = a.seed;
+    sc.thr = (double)__int_as_float(rec(V, R_SPAWN));
+
+    // ---- goals
+    if ((pok & 6) != 6) {
+        u32 PG[32];
+        if (pok & 2) {
+#pragma unroll
+            for (int q = 0; q < 32; q++) PG[q] = mg[q * 64];    // goal planes
+        } else {
+            load_pairs(gg, PG);                                 // goal cells
+            transpose32(PG);
+        }
+        u32 cg[2];
+        if (SL_BITS_ABL & 1) { cg[0] = cg[1] = 0; asm volatile("" : "+v"(PG[0])); }
+        else rule_planes(PG, cg, lane, sc, 1u);
+        const u32 rg = wave_or(cg[0] | cg[1]);
+        if (mg) {      // mirror: the words whose 32 cells changed (all of them if rebuilt)
+            const bool all = !(pok & 2);
+#pragma unroll
+            for (int w = 0; w < 2; w++)
+                if (all || cg[w])
+#pragma unroll
+                    for (int k = 0; k < 16; k++) mg[(k + 16 * w) * 64] = PL(PG, k, w);
+            const bool fixed = rg == 0 && __ballot((PL(PG, 7, 0) | PL(PG, 7, 1)) != 0u) == 0ull;
+            const int ok = 2 | (fixed ? 4 : 0);
+            if (ok != pok && lane == 0) st.planes_ok[b] = ok;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            gcol[k][0] = PL(PG, 9 + k, 0);
+            gcol[k][1] = PL(PG, 9 + k, 1);
+        }
+        if (rg) {
+            transpose32(PG);
+            store_pairs(gg, PG, rg);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- board: from LDS; the start board comes from the level pool (cache) when
+    // the env was reset from it, else from HBM through the same LDS buffer
+    int roll = -1;
+    if (fx.pool.K > 0 && fx.pool.board_planes && st.start_roll) roll = rec(V, R_ROLL);
+    wait_vm();
+
+    // the action (lane 0), on the staged board and the record
+    OverlayT<LdsCells> ov;
+    ov.src.buf = buf;
     ov.n = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         ov.idx[k] = 0;
         ov.val[k] = 0;
     }
-    ActResult ar{0, 0, 0, 0};
-    if (!(SL_BITS_ABL & 16) && (SL_BITS_UACT || lane == 0)) ar = lane_action<false>(st, b, actions[b], ctp, ctc, nullptr, ov);
+    RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
+               rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
+    int act_reward = 0;
+    if (!(SL_BITS_ABL & 16) && (SL_BITS_UACT || lane == 0))
+        act_reward = act_core(env, rec(V, R_ACT), N, N, ctp, ctc, ov);
+    act_reward = __builtin_amdgcn_readfirstlane(act_reward);
     const int ne = __builtin_amdgcn_readfirstlane(ov.n);
-    const int act_reward = __builtin_amdgcn_readfirstlane(ar.reward);
     int eidx[4];
     u32 eval[4];
 #pragma unroll
@@ -600,46 +783,13 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         eidx[k] = __builtin_amdgcn_readfirstlane(ov.idx[k]);
         eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
     }
+    RecFields fl{V, __builtin_amdgcn_readfirstlane(env.go), __builtin_amdgcn_readfirstlane(env.ax),
+                 __builtin_amdgcn_readfirstlane(env.ay), 0.0};
+    if (a.bonus_period > 0)        // issued now, consumed by the epilogue
+        fl.bval = a.bonus_table[bonus_dist(fl.ax, fl.ay, fl.prior_x(fl.prior_head()),
+                                           fl.prior_y(fl.prior_head()), fl.prior_len(),
+                                           a.bonus_period, a.bonus_len)];
 
-    SpawnCtx sc;
-    sc.gid = a.env0 + (uint32_t)b;
-    sc.step = a.step;
-    sc.seed = a.seed;
-    sc.thr = (double)st.spawn_prob[b];
-
-    // ---- goals (independent of the action)
-    if (!(pok & 2)) transpose32(PG);
-    u32 cg[2];
-    if (SL_BITS_ABL & 1) { cg[0] = cg[1] = 0; asm volatile("" : "+v"(PG[0])); }
-    else rule_planes(PG, cg, lane, sc, 1u);
-    if (mg) {      // mirror: the words whose 32 cells changed (all of them if rebuilt)
-        const bool all = !(pok & 2);
-#pragma unroll
-        for (int w = 0; w < 2; w++)
-            if (all || cg[w])
-#pragma unroll
-                for (int k = 0; k < 16; k++) mg[(k + 16 * w) * 64] = PL(PG, k, w);
-        if (!(pok & 2) && lane == 0) st.planes_ok[b] = 2;
-    }
-    const u32 rg = wave_or(cg[0] | cg[1]);
-    u32 gcol[3][2];                    // goal colour planes, kept for the scores
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        gcol[k][0] = PL(PG, 9 + k, 0);
-        gcol[k][1] = PL(PG, 9 + k, 1);
-    }
-    if (rg) {
-        transpose32(PG);
-        store_pairs(gg, PG, rg);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-
-    // ---- board: from LDS; the start board comes from the level pool (cache) when
-    // the env was reset from it, else from HBM through the same LDS buffer
-    int roll = -1;
-    if (fx.pool.K > 0 && fx.pool.board_planes && st.start_roll) roll = st.start_roll[b];
-    roll = __builtin_amdgcn_readfirstlane(roll);
-    wait_vm();
     u32 PB[32];
     read_pairs(buf, lane, PB);
     if (roll < 0) {
@@ -673,7 +823,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     // ---- scores over the new board and goals
     u32 PS[32];
     if (roll >= 0) {
-        pool_planes(fx.pool, __builtin_amdgcn_readfirstlane(st.level_index[b]), roll >> 16,
+        pool_planes(fx.pool, rec(V, R_LI), roll >> 16,
                     roll & 0xFFFF, lane, PS);
     } else {
         wait_vm();
@@ -698,7 +848,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     const int side_total = (s2 >> 16) & 0xFFFF;
     const u32 rb = wave_or(cb[0] | cb[1]) | erow;
     if (rb && !(SL_BITS_ABL & 8)) {
-        const bool can = can_exit_now(st.min_performance[b], score, st.baseline[b], possible);
+        const bool can = can_exit_now(fl.min_performance(), score, fl.baseline(), possible);
 #pragma unroll
         for (int w = 0; w < 2; w++)
             PL(PB, 9, w) = can ? (PL(PB, 9, w) | PL(PB, 8, w)) : (PL(PB, 9, w) & ~PL(PB, 8, w));
@@ -707,8 +857,8 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     }
     int reset = 0;
     if (!(SL_BITS_ABL & 16) && (SL_BITS_UEPI || lane == 0))
-        reset = env_epilogue(st, a, b, act_reward, points, score, possible, side_total,
-                             reward_out, done_out, flags_out, ep_len_out, ep_rew_out);
+        reset = epilogue_core(st, a, b, fl, act_reward, points, score, possible, side_total,
+                              reward_out, done_out, flags_out, ep_len_out, ep_rew_out);
     reset = __builtin_amdgcn_readfirstlane(reset);
     if (fx.fuse_reset && reset && lane == 0) {
         // queue the env for the reset kernel (k_env_reset_list)

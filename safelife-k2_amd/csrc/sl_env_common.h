@@ -43,50 +43,87 @@ __device__ __forceinline__ bool can_exit_now(double mp, int score, int baseline,
     return (double)(score - baseline) >= __dmul_rn(mp, (double)(possible - baseline));
 }
 
+// movement-bonus distance (MovementBonusWrapper.step, env_wrappers.py:72-80): from
+// the oldest ring position, padded by the missing entries while the ring fills;
+// clamped to the table (bonus_table[d] = bonus * (d / n) ** power, host-computed)
+__device__ __forceinline__ int bonus_dist(int ax, int ay, int px, int py, int len, int n,
+                                          int bonus_len) {
+    const int d = (len > 0) ? abs(ax - px) + abs(ay - py) + (len < n ? n - len : 0) : n;
+    return min(d, bonus_len - 1);
+}
+
+// Reads of the per-env fields the epilogue needs, straight from sl_env_state.
+// The 64x64 kernel substitutes a prefetched copy (sl_bits.hip).
+struct GlobalFields {
+    const sl_env_state &st;
+    int64_t b;
+    const double *bonus_table;
+    __device__ int old_points() const { return st.old_points[b]; }
+    __device__ int num_steps() const { return st.num_steps[b]; }
+    __device__ int episode_length() const { return st.episode_length[b]; }
+    __device__ int episode_reward() const { return st.episode_reward[b]; }
+    __device__ double min_performance() const { return st.min_performance[b]; }
+    __device__ int baseline() const { return st.baseline[b]; }
+    __device__ int exit_count() const { return st.exit_count[b]; }
+    __device__ int exit_y(int e) const { return st.exit_y[b * SL_MAX_EXITS + e]; }
+    __device__ int exit_x(int e) const { return st.exit_x[b * SL_MAX_EXITS + e]; }
+    __device__ int game_over() const { return st.game_over[b]; }
+    __device__ int agent_x() const { return st.agent_x[b]; }
+    __device__ int agent_y() const { return st.agent_y[b]; }
+    __device__ int prior_len() const { return st.prior_len[b]; }
+    __device__ int prior_head() const { return st.prior_head[b]; }
+    __device__ int prior_x(int k) const { return st.prior_x[b * SL_BONUS_PERIOD_MAX + k]; }
+    __device__ int prior_y(int k) const { return st.prior_y[b * SL_BONUS_PERIOD_MAX + k]; }
+    __device__ int side_effect() const { return st.side_effect[b]; }
+    __device__ double bonus(int d) const { return bonus_table[d]; }
+};
+
 // Per-env bookkeeping after the board advance.  Executed by one lane, or by a whole
 // wave with wave-uniform arguments (every lane then stores the same values, and the
 // integer work runs on the scalar unit).
+//   f: the env's fields before the bookkeeping (after the action);
 //   points / score / possible / side: the new totals over the advanced board.
 // Mirrors SafeLifeEnv.step (safelife_env.py:160-175), update_exit_colors
 // (safelife_game.py:531-537), MovementBonusWrapper.step (env_wrappers.py:67-88),
 // SimpleSideEffectPenalty.step (env_wrappers.py:319-346) and ContinuingEnv.step
 // (env_wrappers.py:298-303) in that order.
-__device__ __forceinline__ bool env_epilogue(const sl_env_state &st, const StepArgs &a,
-                                             int64_t b, int act_reward, int points, int score,
-                                             int possible, int side, double *reward_out,
-                                             uint8_t *done_out, uint8_t *flags_out,
-                                             int32_t *ep_len_out, int32_t *ep_rew_out) {
+template <class F>
+__device__ __forceinline__ bool epilogue_core(const sl_env_state &st, const StepArgs &a,
+                                              int64_t b, const F &f, int act_reward, int points,
+                                              int score, int possible, int side,
+                                              double *reward_out, uint8_t *done_out,
+                                              uint8_t *flags_out, int32_t *ep_len_out,
+                                              int32_t *ep_rew_out) {
     const int W = st.W;
     uint16_t *gb = st.board + b * (int64_t)st.H * W;
-    const int r_int = act_reward + (points - st.old_points[b]);
+    const int r_int = act_reward + (points - f.old_points());
     st.old_points[b] = points;
-    st.num_steps[b] += 1;
-    const int ep_len = st.episode_length[b] + 1;
-    const int ep_rew = st.episode_reward[b] + r_int;
+    st.num_steps[b] = f.num_steps() + 1;
+    const int ep_len = f.episode_length() + 1;
+    const int ep_rew = f.episode_reward() + r_int;
     st.episode_length[b] = ep_len;
     st.episode_reward[b] = ep_rew;
     st.score[b] = score;
     st.possible[b] = possible;
-    const bool can = can_exit_now(st.min_performance[b], score, st.baseline[b], possible);
+    const bool can = can_exit_now(f.min_performance(), score, f.baseline(), possible);
     const uint16_t ev = (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
-    const int ne = min(st.exit_count[b], SL_MAX_EXITS);
+    const int ne = min(f.exit_count(), SL_MAX_EXITS);
     for (int e = 0; e < ne; e++)      // exits are frozen and never change otherwise
-        gb[st.exit_y[b * SL_MAX_EXITS + e] * W + st.exit_x[b * SL_MAX_EXITS + e]] = ev;
+        gb[f.exit_y(e) * W + f.exit_x(e)] = ev;
     const bool times_up = ep_len > a.time_limit;
-    const bool over = st.game_over[b] != 0;
+    const bool over = f.game_over() != 0;
     const bool completed = times_up || over;
 
     double r = (double)r_int;
     if (a.bonus_period > 0) {
         const int n = a.bonus_period;
-        const int len = st.prior_len[b], head = st.prior_head[b];
-        const int ax = st.agent_x[b], ay = st.agent_y[b];
+        const int len = f.prior_len(), head = f.prior_head();
+        const int ax = f.agent_x(), ay = f.agent_y();
         int32_t *px = st.prior_x + b * SL_BONUS_PERIOD_MAX;
         int32_t *py = st.prior_y + b * SL_BONUS_PERIOD_MAX;
-        int dist = (len > 0) ? abs(ax - px[head]) + abs(ay - py[head]) + (len < n ? n - len : 0)
-                             : n;
-        dist = min(dist, a.bonus_len - 1);
-        r = __dadd_rn(r, a.bonus_table[dist]);
+        const int dist = bonus_dist(ax, ay, f.prior_x(head), f.prior_y(head), len, n,
+                                    a.bonus_len);
+        r = __dadd_rn(r, f.bonus(dist));
         if (len < n) {
             const int slot = head + len >= n ? head + len - n : head + len;   // head, len < n
             px[slot] = ax;
@@ -100,7 +137,7 @@ __device__ __forceinline__ bool env_epilogue(const sl_env_state &st, const StepA
     }
     // reward -= delta_effect * coef: a rounded product, then a rounded difference
     // (an fma here would differ from Python in the last bit)
-    r = __dsub_rn(r, __dmul_rn((double)(side - st.side_effect[b]), a.penalty_coef));
+    r = __dsub_rn(r, __dmul_rn((double)(side - f.side_effect()), a.penalty_coef));
     st.side_effect[b] = side;
 
     reward_out[b] = r;
@@ -111,6 +148,16 @@ __device__ __forceinline__ bool env_epilogue(const sl_env_state &st, const StepA
     if (ep_len_out) ep_len_out[b] = completed ? ep_len : 0;
     if (ep_rew_out) ep_rew_out[b] = completed ? ep_rew : 0;
     return a.auto_reset && completed;      // the env is reset after this step
+}
+
+__device__ __forceinline__ bool env_epilogue(const sl_env_state &st, const StepArgs &a,
+                                             int64_t b, int act_reward, int points, int score,
+                                             int possible, int side, double *reward_out,
+                                             uint8_t *done_out, uint8_t *flags_out,
+                                             int32_t *ep_len_out, int32_t *ep_rew_out) {
+    return epilogue_core(st, a, b, GlobalFields{st, b, a.bonus_table}, act_reward, points,
+                         score, possible, side, reward_out, done_out, flags_out, ep_len_out,
+                         ep_rew_out);
 }
 
 // ---------------------------------------------------------------------------

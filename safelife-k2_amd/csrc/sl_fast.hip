@@ -373,7 +373,7 @@ k_env_step_w64(sl_env_state st, StepArgs a, const int32_t *__restrict__ actions,
     // -- the action, on lane 0 (its cell reads overlap the row loads above)
     ActResult ar{0, 0, 0, 0};
     Overlay ov;
-    ov.bd = st.board + off;
+    ov.src.bd = st.board + off;
     ov.n = 0;
     if (lane == 0) ar = lane_action(st, b, actions[b], ctp, ctc, &tbl, ov);
     Edits ed;
@@ -528,7 +528,7 @@ k_env_step_w64_lds(sl_env_state st, StepArgs a, const int32_t *__restrict__ acti
     // not ready before the barrier), while the copies are in flight
     ActResult ar{0, 0, 0, 0};
     Overlay ov;
-    ov.bd = st.board + off;
+    ov.src.bd = st.board + off;
     ov.n = 0;
     if (threadIdx.x == 0) ar = lane_action(st, b, actions[b], ctp, ctc, nullptr, ov);
     __builtin_amdgcn_s_waitcnt(0);
