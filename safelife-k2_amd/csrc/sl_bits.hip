@@ -412,27 +412,42 @@ __device__ __forceinline__ void read_pairs(const lds_u32 *buf, int lane, u32 D[3
 // level li rolled by (dy, dx) (sl_env_state.start_roll).  Column c of the start
 // board is level column c - dx; its 64-bit row column rotated by dy gives rows
 // 32h .. 32h+31 as one funnel shift.  The pool stays in L2 / the Infinity Cache,
-// so this costs no HBM traffic and no transpose.
-__device__ __forceinline__ void pool_planes(const sl_level_pool &pool, int li, int dy, int dx,
-                                            int lane, u32 S[32]) {
-    const uint2 *pl = reinterpret_cast<const uint2 *>(pool.board_planes) + (int64_t)li * 16 * N;
+// so this costs no HBM traffic and no transpose.  The level's planes 0-3 and 6-15
+// (7 KiB, seven 1 KiB DMA rows) are copied into the wave's board buffer as soon as
+// the board has been read out of it, so their (queueing-dominated) latency runs
+// under the action and the rule (issued at scoring time, it was ~40% of a wave's
+// life; held in registers instead, it spills).
+__device__ __forceinline__ void pool_dma(const sl_level_pool &pool, int li, lds_u32 *buf,
+                                         int lane) {
+    const char *pl = reinterpret_cast<const char *>(pool.board_planes + (int64_t)li * 16 * N);
+#pragma unroll
+    for (int k = 0; k < 7; k++) {       // LDS row k <- planes (0,1), (2,3), (6,7) .. (14,15)
+        const int p0 = k < 2 ? 2 * k : 2 * k + 2;
+        __builtin_amdgcn_global_load_lds((const void *)(pl + p0 * N * 8 + lane * 16),
+                                         (__attribute__((address_space(3))) void *)(buf + k * 256),
+                                         16, 0, 0);
+    }
+}
+__device__ __forceinline__ void pool_planes_lds(const lds_u32 *buf, int dy, int dx, int lane,
+                                                u32 S[32]) {
     const int c0 = (2 * (lane >> 1) - dx) & 63, c1 = (c0 + 1) & 63;
-    // bits 32h .. 32h+31 of rotl64(v, dy) = bits r .. r+31 of v, r = (32h - dy) mod 64
     const int r = (32 * (lane & 1) - dy) & 63;
     const bool lo_first = r < 32;
     const u32 sh = (u32)(r & 31);
 #pragma unroll
     for (int p = 0; p < 16; p++) {
-        if (p == 1 || (p >= 3 && p <= 6)) {        // player bits: not compared
+        if (p == 1 || (p >= 3 && p <= 6)) {
             PL(S, p, 0) = 0u;
             PL(S, p, 1) = 0u;
             continue;
         }
-        const uint2 v0 = pl[p * N + c0], v1 = pl[p * N + c1];
-        PL(S, p, 0) = lo_first ? __builtin_amdgcn_alignbit(v0.y, v0.x, sh)
-                               : __builtin_amdgcn_alignbit(v0.x, v0.y, sh);
-        PL(S, p, 1) = lo_first ? __builtin_amdgcn_alignbit(v1.y, v1.x, sh)
-                               : __builtin_amdgcn_alignbit(v1.x, v1.y, sh);
+        const int slot = p < 4 ? p : p - 2;             // LDS plane slot
+        const lds_u32 *q = buf + slot * 128;            // 64 columns x 2 dwords
+        const u32 a0 = q[2 * c0], a1 = q[2 * c0 + 1], b0 = q[2 * c1], b1 = q[2 * c1 + 1];
+        PL(S, p, 0) = lo_first ? __builtin_amdgcn_alignbit(a1, a0, sh)
+                               : __builtin_amdgcn_alignbit(a0, a1, sh);
+        PL(S, p, 1) = lo_first ? __builtin_amdgcn_alignbit(b1, b0, sh)
+                               : __builtin_amdgcn_alignbit(b0, b1, sh);
     }
 }
 
@@ -792,10 +807,9 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
 
     u32 PB[32];
     read_pairs(buf, lane, PB);
-    if (roll < 0) {
-        wait_lgkm();
-        dma_board(st.start_board + off, buf, lane);
-    }
+    wait_lgkm();
+    if (roll < 0) dma_board(st.start_board + off, buf, lane);
+    else pool_dma(fx.pool, rec(V, R_LI), buf, lane);
     transpose32(PB);
     u32 erow = 0;                      // row pairs (y, y + 32) holding an edit
 #pragma unroll
@@ -822,11 +836,10 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
 
     // ---- scores over the new board and goals
     u32 PS[32];
+    wait_vm();
     if (roll >= 0) {
-        pool_planes(fx.pool, rec(V, R_LI), roll >> 16,
-                    roll & 0xFFFF, lane, PS);
+        pool_planes_lds(buf, roll >> 16, roll & 0xFFFF, lane, PS);
     } else {
-        wait_vm();
         read_pairs(buf, lane, PS);
         transpose32(PS);
     }
