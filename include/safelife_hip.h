@@ -50,7 +50,8 @@ extern "C" {
 #define SL_RNG_STREAM 0     /* replay a supplied uniform stream (reference order) */
 #define SL_RNG_PHILOX 1     /* counter-based Philox4x32-10 (production) */
 
-#define SL_KERNEL_AUTO 0     /* bit-sliced kernel for 64x64 in Philox mode */
+#define SL_KERNEL_AUTO 0     /* bit-sliced kernels for 64x64 and 128x128 in
+                                Philox mode, the generic kernel otherwise    */
 #define SL_KERNEL_GENERIC 1  /* LDS-staged per-cell kernel, any shape        */
 #define SL_KERNEL_FAST 2     /* require the fast kernel (error if none)      */
 
@@ -170,11 +171,16 @@ typedef struct sl_env_state {
                                  every reset); -1: start_board was written by
                                  the caller.  Lets the 64x64 kernel read the
                                  start board from the cache-resident pool.     */
-    uint32_t *planes;         /* [B,2,32,64] or NULL (64x64 only): bit-plane
-                                 mirror of the goals (half 1; half 0 reserved)
-                                 kept by the 64x64 kernel: [b][1][q][lane],
-                                 word q = plane q & 15 of column 2(lane>>1) +
-                                 (q>>4), rows 32(lane&1)..+31 (sl_bits.hip).
+    uint32_t *planes;         /* bit-plane mirror of the goals kept by the
+                                 bit-sliced kernels, or NULL (then 128x128
+                                 boards take the generic kernel).
+                                 64x64: [B,2,32,64], half 1 (half 0 reserved):
+                                 [b][1][q][lane], word q = plane q & 15 of
+                                 column 2(lane>>1) + (q>>4), rows
+                                 32(lane&1)..+31 (sl_bits.hip).
+                                 128x128: [B,4,32,64], [b][t][q][lane], word q
+                                 = plane q & 15 of column 2 lane + (q>>4),
+                                 rows 32t..32t+31 (sl_bits128.hip).
                                  Derived data, never read unless planes_ok
                                  bit 1 is set.                                 */
     int32_t *planes_ok;       /* [B] bit1: goals mirror valid; bit2: goals at

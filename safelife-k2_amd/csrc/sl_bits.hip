@@ -29,14 +29,13 @@
 // written into the planes before the rule.  Envs that finish are queued; a second
 // kernel (k_env_reset_list) resets exactly those, one wave each, so the step
 // kernel carries no reset code (121 VGPRs, 4 waves/SIMD, no spills).
-#include "sl_action.h"
+#include "sl_bits.h"
 
 using namespace sl;
 using namespace sl::fast;
+using namespace sl::bits;
 
 namespace {
-
-typedef uint32_t u32;
 
 #ifndef SL_BITS_WPB
 #define SL_BITS_WPB 1        // envs (waves) per workgroup
@@ -62,323 +61,26 @@ typedef uint32_t u32;
 
 constexpr int N = 64;        // rows = columns = lanes
 
-// ---------------------------------------------------------------- primitives
-__device__ __forceinline__ u32 maj(u32 a, u32 b, u32 c) { return (a & b) | (c & (a | b)); }
-__device__ __forceinline__ u32 mux(u32 s, u32 a, u32 b) { return (s & a) | (~s & b); }
-
-// whole-wave lane rotations (wrap at 64 lanes); every lane has a source, so no old value
-__device__ __forceinline__ u32 lane_m1(u32 v) {      // value of lane l - 1
-    return (u32)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xF, 0xF, false);  // wave_ror:1
-}
-__device__ __forceinline__ u32 lane_p1(u32 v) {      // value of lane l + 1
-    return (u32)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xF, 0xF, false);  // wave_rol:1
-}
-__device__ __forceinline__ u32 lane_x1(u32 v) {      // value of lane l ^ 1 (the other half)
-    return (u32)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-}
-
-// the three columns around each of the lane's two columns: word w of a plane is
-// column 2j + w, so column 2j - 1 is word 1 of lane l - 2 and column 2j + 2 is
-// word 0 of lane l + 2 (the same half; the 64-lane rotation wraps at W = 64)
-struct H3 {
-    u32 l0, r1;          // column 2j - 1, column 2j + 2
+// Neighbourhood of the 64x64 layout: lane l holds columns 2j, 2j+1 (j = l >> 1) over
+// rows 32h .. 32h+31 (h = l & 1).  Column 2j - 1 is word 1 of lane l - 2 and column
+// 2j + 2 word 0 of lane l + 2 (the 64-lane rotation wraps at W = 64); the rows
+// around a word come from the other half's word (lane l ^ 1), which also supplies
+// the wrap at H = 64.
+struct Geo64 {
+    int lane;
+    template <class F>
+    __device__ __forceinline__ V3 vert(const u32 *P, int w, F f) const {
+        const u32 x = f(P, w);
+        return vert_with(x, lane_x1(x));
+    }
+    __device__ __forceinline__ H3 horiz(u32 w0, u32 w1) const {
+        return H3{lane_m1(lane_m1(w1)), lane_p1(lane_p1(w0))};
+    }
+    __device__ __forceinline__ bool halo_spawn() const { return false; }
+    __device__ __forceinline__ u32 cell(int y, int w) const {
+        return (u32)((32 * (lane & 1) + y) * N + 2 * (lane >> 1) + w);
+    }
 };
-__device__ __forceinline__ H3 horiz(u32 w0, u32 w1) {
-    return H3{lane_m1(lane_m1(w1)), lane_p1(lane_p1(w0))};
-}
-
-// rows y - 1 and y + 1 of a lane's 32-row word (the other half supplies the wrap)
-struct V3 {
-    u32 up, dn;
-};
-__device__ __forceinline__ V3 vert(u32 x) {
-    const u32 o = lane_x1(x);
-    return V3{__builtin_amdgcn_alignbit(x, o, 31u), __builtin_amdgcn_alignbit(o, x, 1u)};
-}
-
-template <int J, u32 M>
-__device__ __forceinline__ void swap_stage(u32 A[32]) {
-#pragma unroll
-    for (int k = 0; k < 32; k++)
-        if (!(k & J)) {
-            const u32 a = A[k], b = A[k + J];
-            A[k] = (M & a) | (~M & (b << J));
-            A[k + J] = (M & (a >> J)) | (~M & b);
-        }
-}
-
-// in-place 32x32 bit transpose: bit y of A'[c] = bit c of A[y] (an involution)
-__device__ __forceinline__ void transpose32(u32 A[32]) {
-#pragma unroll
-    for (int k = 0; k < 16; k++) {      // 16-bit halves
-        const u32 a = A[k], b = A[k + 16];
-        A[k] = __builtin_amdgcn_perm(b, a, 0x05040100u);
-        A[k + 16] = __builtin_amdgcn_perm(b, a, 0x07060302u);
-    }
-#pragma unroll
-    for (int g = 0; g < 32; g += 16)    // bytes
-#pragma unroll
-        for (int k = g; k < g + 8; k++) {
-            const u32 a = A[k], b = A[k + 8];
-            A[k] = __builtin_amdgcn_perm(b, a, 0x06020400u);
-            A[k + 8] = __builtin_amdgcn_perm(b, a, 0x07030501u);
-        }
-    swap_stage<4, 0x0F0F0F0Fu>(A);
-    swap_stage<2, 0x33333333u>(A);
-    swap_stage<1, 0x55555555u>(A);
-}
-
-// plane k, word w of a transposed column
-#define PL(P, k, w) P[(k) + 16 * (w)]
-
-// p points at the lane's first dword (row 32h, columns 2j, 2j+1); rows are 32 dwords
-__device__ __forceinline__ void load_pairs(const u32 *__restrict__ p, u32 D[32]) {
-#pragma unroll
-    for (int y = 0; y < 32; y++) D[y] = p[y * 32];
-}
-
-template <int CTRL>
-__device__ __forceinline__ u32 dpp(u32 v) {
-    return (u32)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
-}
-__device__ __forceinline__ int wave_total(int x) {
-    u32 v = (u32)x;
-    v += dpp<0xB1>(v);
-    v += dpp<0x4E>(v);
-    v += dpp<0x141>(v);
-    v += dpp<0x140>(v);
-    return (int)((u32)__builtin_amdgcn_readlane((int)v, 0) + (u32)__builtin_amdgcn_readlane((int)v, 16) +
-                 (u32)__builtin_amdgcn_readlane((int)v, 32) + (u32)__builtin_amdgcn_readlane((int)v, 48));
-}
-__device__ __forceinline__ u32 wave_or(u32 v) {
-    v |= dpp<0xB1>(v);
-    v |= dpp<0x4E>(v);
-    v |= dpp<0x141>(v);
-    v |= dpp<0x140>(v);
-    return (u32)__builtin_amdgcn_readlane((int)v, 0) | (u32)__builtin_amdgcn_readlane((int)v, 16) |
-           (u32)__builtin_amdgcn_readlane((int)v, 32) | (u32)__builtin_amdgcn_readlane((int)v, 48);
-}
-
-// ---------------------------------------------------------------- the rule
-struct SpawnCtx {
-    uint32_t gid, step;
-    uint64_t seed;
-    double thr;
-};
-
-// One CA step of the 64x64 column planes P (in place).  chg[w] = cells that changed.
-// Appendix A: alive x survives iff frozen | P | cnt in {3,4}; dead x unless frozen | I
-// is born iff cnt == 3 (colours: >= 2 alive of a colour, or any spawner of it;
-// destructible: >= 2 alive destructible-or-exit), else spawns with probability p
-// when a spawner is in the block.  Births and spawns clear every other bit.
-// The spawner terms (spawner colours, the draws) are a second phase that only runs
-// when the wave's planes hold a spawning cell, so the common path stays lean.
-__device__ __forceinline__ void rule_planes(u32 P[32], u32 chg[2], int lane, const SpawnCtx &sc,
-                                            u32 tensor) {
-    // Each 3x3 quantity is folded vertically (rows y-1, y, y+1 of the lane's word)
-    // and then horizontally (word 0 sees columns 2j-1, 2j, 2j+1; word 1 sees 2j,
-    // 2j+1, 2j+2), one quantity at a time so only the reduced results stay live.
-    u32 eq3[2], eq34[2];
-    {   // 9-cell alive count: 3-row sums s = s0 + 2 s1, then t0 + 2h over 3 columns
-        u32 s0[2], s1[2];
-#pragma unroll
-        for (int w = 0; w < 2; w++) {
-            const u32 a = PL(P, 0, w);
-            const V3 v = vert(a);
-            s0[w] = v.up ^ a ^ v.dn;
-            s1[w] = maj(v.up, a, v.dn);
-        }
-        const H3 h0 = horiz(s0[0], s0[1]), h1 = horiz(s1[0], s1[1]);
-#pragma unroll
-        for (int w = 0; w < 2; w++) {
-            const u32 L0 = w ? s0[0] : h0.l0, R0 = w ? h0.r1 : s0[1];
-            const u32 L1 = w ? s1[0] : h1.l0, R1 = w ? h1.r1 : s1[1];
-            const u32 t0 = L0 ^ s0[w] ^ R0, c0 = maj(L0, s0[w], R0);
-            const u32 a1 = L1 ^ s1[w] ^ R1, b1 = maj(L1, s1[w], R1);
-            const u32 hh1 = ~b1 & (a1 ^ c0);                         // h == 1
-            const u32 hh2 = (b1 & ~a1 & ~c0) | (~b1 & a1 & c0);      // h == 2
-            eq3[w] = t0 & hh1;
-            eq34[w] = mux(t0, hh1, hh2);
-        }
-    }
-    // >= 2 of the 9 cells: alive & (destructible | exit), alive & colour k
-    u32 two[4][2];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        u32 o[2], t[2];
-#pragma unroll
-        for (int w = 0; w < 2; w++) {
-            const u32 a = PL(P, 0, w);
-            const u32 x = q == 0 ? a & (PL(P, 3, w) | PL(P, 8, w)) : a & PL(P, 8 + q, w);
-            const V3 v = vert(x);
-            o[w] = v.up | x | v.dn;
-            t[w] = maj(v.up, x, v.dn);
-        }
-        const H3 ho = horiz(o[0], o[1]), ht = horiz(t[0], t[1]);
-        two[q][0] = ht.l0 | t[0] | t[1] | maj(ho.l0, o[0], o[1]);
-        two[q][1] = t[0] | t[1] | ht.r1 | maj(o[0], o[1], ho.r1);
-    }
-    // any of the 9 cells: preserve, inhibit, spawn
-    u32 any[3][2];
-#pragma unroll
-    for (int f = 0; f < 3; f++) {
-        u32 o[2];
-#pragma unroll
-        for (int w = 0; w < 2; w++) {
-            const u32 x = PL(P, 5 + f, w);
-            const V3 v = vert(x);
-            o[w] = v.up | x | v.dn;
-        }
-        const H3 h = horiz(o[0], o[1]);
-        any[f][0] = h.l0 | o[0] | o[1];
-        any[f][1] = o[0] | o[1] | h.r1;
-    }
-    u32 kill[2], birth[2], pairD[2], colk[3][2], elig[2];
-#pragma unroll
-    for (int w = 0; w < 2; w++) {
-        const u32 A = PL(P, 0, w), F = PL(P, 4, w);
-        kill[w] = A & ~(F | any[0][w] | eq34[w]);
-        const u32 dead_ok = ~(A | F | any[1][w]);
-        birth[w] = dead_ok & eq3[w];
-        pairD[w] = two[0][w];
-#pragma unroll
-        for (int k = 0; k < 3; k++) colk[k][w] = two[1 + k][w];
-        elig[w] = dead_ok & ~eq3[w] & any[2][w];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- spawner phase: spawner colours reach every newborn; eligible cells draw
-    u32 sp[2] = {0u, 0u};
-    if (__ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull) {     // 64-bit wave mask
-        u32 vsc[3][2];
-#pragma unroll
-        for (int k = 0; k < 3; k++)
-#pragma unroll
-            for (int w = 0; w < 2; w++) {
-                const u32 x = PL(P, 7, w) & PL(P, 9 + k, w);
-                const V3 v = vert(x);
-                vsc[k][w] = v.up | x | v.dn;
-            }
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            const H3 h = horiz(vsc[k][0], vsc[k][1]);
-            colk[k][0] |= h.l0 | vsc[k][0] | vsc[k][1];
-            colk[k][1] |= vsc[k][0] | vsc[k][1] | h.r1;
-        }
-        const int row0 = 32 * (lane & 1), col0 = 2 * (lane >> 1);
-#pragma unroll
-        for (int w = 0; w < 2; w++) {
-            u32 e = elig[w], s = 0;
-            while (e) {
-                const int y = __builtin_ctz(e);
-                e &= e - 1;
-                const u32 cell = (u32)((row0 + y) * N + col0 + w);
-                if (philox_uniform(cell, sc.gid, sc.step, tensor, sc.seed) < sc.thr) s |= 1u << y;
-            }
-            sp[w] = s;
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- new planes
-#pragma unroll
-    for (int w = 0; w < 2; w++) {
-        const u32 c = kill[w] | birth[w] | sp[w];
-        const u32 born = birth[w] | sp[w];
-        chg[w] = c;
-        PL(P, 0, w) ^= c;
-        PL(P, 3, w) = mux(c, (birth[w] & pairD[w]) | sp[w], PL(P, 3, w));
-#pragma unroll
-        for (int k = 0; k < 3; k++) PL(P, 9 + k, w) = mux(c, born & colk[k][w], PL(P, 9 + k, w));
-        PL(P, 1, w) &= ~c;
-        PL(P, 2, w) &= ~c;
-#pragma unroll
-        for (int k = 4; k <= 8; k++) PL(P, k, w) &= ~c;
-#pragma unroll
-        for (int k = 12; k <= 15; k++) PL(P, k, w) &= ~c;
-    }
-}
-
-// ---------------------------------------------------------------- scoring
-// point_table (safelife_game.py:554-565) as compile-time column sets per value class
-__host__ __device__ constexpr int pt_value(int g, int c) {
-    constexpr int8_t t[64] = {0,  -1, 0,  0, 0,  0, 0,  0,  -3, 3,  -3, 0, -3, 0, -3, -3,
-                              0,  -3, 5,  0, 0,  0, 3,  0,  -3, 0,  0,  3, 0,  0, 0,  0,
-                              3,  -3, 3,  0, 5,  3, 3,  3,  -3, 3,  -3, 0, -3, 5, -3, -3,
-                              3,  -3, 3,  0, 3,  0, 5,  3,  0,  -1, 0,  0, 0,  0, 0,  0};
-    return t[g * 8 + c];
-}
-__host__ __device__ constexpr int pt_set(int g, int v) {
-    int s = 0;
-    for (int c = 0; c < 8; c++)
-        if (pt_value(g, c) == v) s |= 1 << c;
-    return s;
-}
-
-__device__ __forceinline__ u32 minterm(u32 c0, u32 c1, u32 c2, int i) {
-    return ((i & 1) ? c0 : ~c0) & ((i & 2) ? c1 : ~c1) & ((i & 4) ? c2 : ~c2);
-}
-// cells whose colour index lies in the compile-time set s
-__device__ __forceinline__ u32 colour_in(u32 c0, u32 c1, u32 c2, int s) {
-    u32 r = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-        if ((s >> i) & 1) r |= minterm(c0, c1, c2, i);
-    return r;
-}
-
-struct Totals {
-    int points, score, possible, side;
-};
-
-// Full sums over the board (B: board planes, gc: goal colour planes, S: start-board planes):
-//   points   = sum point_table[g, c] * alive                      (safelife_game.py:590-599)
-//   score    = sum sign(point_table)[g, c] * m,  m = alive & !(frozen & !movable)  (:601-631)
-//   possible = sum [g not in {black, white}]
-//   side     = #cells that are a side effect                      (env_wrappers.py:326-342)
-__device__ __forceinline__ void score_planes(const u32 B[32], const u32 gc[3][2], const u32 S[32],
-                                             int *pts, int *scr, int *pos, int *side) {
-    int p = 0, q = 0, r = 0, e = 0;
-#pragma unroll
-    for (int w = 0; w < 2; w++) {
-        const u32 c0 = PL(B, 9, w), c1 = PL(B, 10, w), c2 = PL(B, 11, w);
-        const u32 g0 = gc[0][w], g1 = gc[1][w], g2 = gc[2][w];
-        u32 m5 = 0, m3 = 0, m1 = 0, mm3 = 0;
-#pragma unroll
-        for (int g = 0; g < 8; g++) {
-            const u32 gm = minterm(g0, g1, g2, g);
-            if (pt_set(g, 5)) m5 |= gm & colour_in(c0, c1, c2, pt_set(g, 5));
-            if (pt_set(g, 3)) m3 |= gm & colour_in(c0, c1, c2, pt_set(g, 3));
-            if (pt_set(g, -1)) m1 |= gm & colour_in(c0, c1, c2, pt_set(g, -1));
-            if (pt_set(g, -3)) mm3 |= gm & colour_in(c0, c1, c2, pt_set(g, -3));
-        }
-        const u32 A = PL(B, 0, w);
-        p += 5 * __builtin_popcount(A & m5) + 3 * __builtin_popcount(A & m3) -
-             __builtin_popcount(A & m1) - 3 * __builtin_popcount(A & mm3);
-        const u32 m = A & ~(PL(B, 4, w) & ~(PL(B, 2, w) | PL(B, 15, w)));
-        q += __builtin_popcount(m & (m5 | m3)) - __builtin_popcount(m & (m1 | mm3));
-        r += __builtin_popcount((g0 ^ g1) | (g0 ^ g2));
-        // side effects: b, s without the player bits; exits compare equal
-        u32 d = PL(B, 0, w) ^ PL(S, 0, w);
-        d |= PL(B, 2, w) ^ PL(S, 2, w);
-#pragma unroll
-        for (int k = 7; k < 16; k++) d |= PL(B, k, w) ^ PL(S, k, w);
-        const u32 start_red_gone = PL(S, 0, w) & PL(S, 9, w) & ~(PL(B, 0, w) & PL(B, 9, w));
-        const u32 blue_goal_alive = g2 & ~g1 & ~g0 & PL(B, 0, w) & ~PL(B, 9, w);
-        e += __builtin_popcount(d & ~PL(S, 8, w) & ~start_red_gone & ~blue_goal_alive);
-    }
-    *pts = p;
-    *scr = q;
-    *pos = r;
-    *side = e;
-}
-
-// ---------------------------------------------------------------- stores
-// the lane's rows y with bit y of rm set (both halves: rm is a wave-wide union) are
-// written back, one dword (two cells) per lane
-__device__ __forceinline__ void store_pairs(u32 *__restrict__ p, const u32 D[32], u32 rm) {
-#pragma unroll
-    for (int y = 0; y < 32; y++)
-        if ((rm >> y) & 1u) p[y * 32] = D[y];
-}
 
 // ---------------------------------------------------------------- LDS staging
 // A wave's 8 KiB LDS buffer holds one 64x64 board, row-major, with the 16-byte
@@ -451,122 +153,6 @@ __device__ __forceinline__ void pool_planes_lds(const lds_u32 *buf, int dy, int 
     }
 }
 
-__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-// ---------------------------------------------------------------- per-env record
-// The per-env fields the action, the spawn/start terms and the epilogue read are
-// fetched by ONE load instruction at kernel start: lane k of the record register
-// holds dword k below, and every later read is a v_readlane.  The lane-0 action and
-// epilogue then wait on no dependent HBM round trips (agent position -> cells,
-// ring head -> ring entry -> bonus); before, those chains cost ~27% of the kernel.
-enum : int {
-    R_ACT = 0, R_GO, R_AX, R_AY, R_SCORE, R_BASE, R_POSS, R_SPAWN, R_ROLL, R_LI, R_OLDP,
-    R_NSTEPS, R_EPLEN, R_EPREW, R_EXC, R_PLEN, R_PHEAD, R_SIDE, R_POK,
-    R_MP = 19,           // min_performance, 2 dwords
-    R_EY = 21,           // exit_y[8] (int16), 4 dwords
-    R_EX = 25,           // exit_x[8], 4 dwords
-    R_PX = 32,           // prior_x[16]
-    R_PY = 48            // prior_y[16]
-};
-
-__device__ __forceinline__ u32 load_record(const sl_env_state &st, const int32_t *actions,
-                                           int64_t b, int lane) {
-    const char *p = reinterpret_cast<const char *>(st.game_over);      // spare lanes
-    int64_t off = b * 4;
-#define SL_SEL(k, ptr)                                                                    \
-    if ((ptr) != nullptr) p = lane == (k) ? reinterpret_cast<const char *>(ptr) : p
-    SL_SEL(R_ACT, actions);
-    SL_SEL(R_AX, st.agent_x);
-    SL_SEL(R_AY, st.agent_y);
-    SL_SEL(R_SCORE, st.score);
-    SL_SEL(R_BASE, st.baseline);
-    SL_SEL(R_POSS, st.possible);
-    SL_SEL(R_SPAWN, st.spawn_prob);
-    SL_SEL(R_ROLL, st.start_roll);
-    SL_SEL(R_LI, st.level_index);
-    SL_SEL(R_OLDP, st.old_points);
-    SL_SEL(R_NSTEPS, st.num_steps);
-    SL_SEL(R_EPLEN, st.episode_length);
-    SL_SEL(R_EPREW, st.episode_reward);
-    SL_SEL(R_EXC, st.exit_count);
-    SL_SEL(R_PLEN, st.prior_len);
-    SL_SEL(R_PHEAD, st.prior_head);
-    SL_SEL(R_SIDE, st.side_effect);
-    SL_SEL(R_POK, st.planes_ok);
-#undef SL_SEL
-    if (lane >= R_MP && lane < R_MP + 2) {
-        p = reinterpret_cast<const char *>(st.min_performance);
-        off = b * 8 + 4 * (lane - R_MP);
-    } else if (lane >= R_EY && lane < R_EY + 4) {
-        p = reinterpret_cast<const char *>(st.exit_y);
-        off = b * 16 + 4 * (lane - R_EY);
-    } else if (lane >= R_EX && lane < R_EX + 4) {
-        p = reinterpret_cast<const char *>(st.exit_x);
-        off = b * 16 + 4 * (lane - R_EX);
-    } else if (lane >= R_PX) {
-        p = reinterpret_cast<const char *>(lane < R_PY ? st.prior_x : st.prior_y);
-        off = b * 64 + 4 * ((lane - R_PX) & 15);
-    }
-    return *reinterpret_cast<const u32 *>(p + off);
-}
-
-__device__ __forceinline__ int rec(u32 V, int k) { return __builtin_amdgcn_readlane((int)V, k); }
-__device__ __forceinline__ double rec_f64(u32 V, int k) {
-    return __hiloint2double(rec(V, k + 1), rec(V, k));
-}
-
-// the action's view of the env: record fields in, state writes out
-struct RecEnv {
-    const sl_env_state &st;
-    int64_t b;
-    int go, ax, ay, score, base, poss;
-    double mp;
-    __device__ int game_over() const { return go; }
-    __device__ int agent_x() const { return ax; }
-    __device__ int agent_y() const { return ay; }
-    __device__ bool can_exit() const { return can_exit_now(mp, score, base, poss); }
-    __device__ void set_orientation(int o) { st.orientation[b] = o; }
-    __device__ void set_game_over() {
-        go = 1;
-        st.game_over[b] = 1;
-    }
-    __device__ void set_agent(int x, int y) {
-        ax = x;
-        ay = y;
-        st.agent_x[b] = x;
-        st.agent_y[b] = y;
-    }
-};
-
-// the epilogue's view (epilogue_core): record fields plus the post-action agent
-struct RecFields {
-    u32 V;
-    int go, ax, ay;
-    double bval;
-    __device__ int old_points() const { return rec(V, R_OLDP); }
-    __device__ int num_steps() const { return rec(V, R_NSTEPS); }
-    __device__ int episode_length() const { return rec(V, R_EPLEN); }
-    __device__ int episode_reward() const { return rec(V, R_EPREW); }
-    __device__ double min_performance() const { return rec_f64(V, R_MP); }
-    __device__ int baseline() const { return rec(V, R_BASE); }
-    __device__ int exit_count() const { return rec(V, R_EXC); }
-    __device__ int exit_y(int e) const {
-        return (int)(int16_t)(rec(V, R_EY + (e >> 1)) >> (16 * (e & 1)));
-    }
-    __device__ int exit_x(int e) const {
-        return (int)(int16_t)(rec(V, R_EX + (e >> 1)) >> (16 * (e & 1)));
-    }
-    __device__ int game_over() const { return go; }
-    __device__ int agent_x() const { return ax; }
-    __device__ int agent_y() const { return ay; }
-    __device__ int prior_len() const { return rec(V, R_PLEN); }
-    __device__ int prior_head() const { return rec(V, R_PHEAD); }
-    __device__ int prior_x(int k) const { return rec(V, R_PX + k); }
-    __device__ int prior_y(int k) const { return rec(V, R_PY + k); }
-    __device__ int side_effect() const { return rec(V, R_SIDE); }
-    __device__ double bonus(int) const { return bval; }
-};
 
 // unedited cells for the action, from the staged board (dma_board's layout)
 typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
@@ -739,12 +325,12 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
 #pragma unroll
             for (int q = 0; q < 32; q++) PG[q] = mg[q * 64];    // goal planes
         } else {
-            load_pairs(gg, PG);                                 // goal cells
+            load_pairs<32>(gg, PG);                                 // goal cells
             transpose32(PG);
         }
         u32 cg[2];
         if (SL_BITS_ABL & 1) { cg[0] = cg[1] = 0; asm volatile("" : "+v"(PG[0])); }
-        else rule_planes(PG, cg, lane, sc, 1u);
+        else rule_planes(PG, cg, Geo64{lane}, sc, 1u);
         const u32 rg = wave_or(cg[0] | cg[1]);
         if (mg) {      // mirror: the words whose 32 cells changed (all of them if rebuilt)
             const bool all = !(pok & 2);
@@ -764,7 +350,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         }
         if (rg) {
             transpose32(PG);
-            store_pairs(gg, PG, rg);
+            store_pairs<32>(gg, PG, rg);
         }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -831,7 +417,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     }
     u32 cb[2];
     if (SL_BITS_ABL & 2) { cb[0] = PB[0] & 1; cb[1] = 0; }
-    else rule_planes(PB, cb, lane, sc, 0u);
+    else rule_planes(PB, cb, Geo64{lane}, sc, 0u);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- scores over the new board and goals
@@ -866,7 +452,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         for (int w = 0; w < 2; w++)
             PL(PB, 9, w) = can ? (PL(PB, 9, w) | PL(PB, 8, w)) : (PL(PB, 9, w) & ~PL(PB, 8, w));
         transpose32(PB);
-        store_pairs(gb, PB, rb);
+        store_pairs<32>(gb, PB, rb);
     }
     int reset = 0;
     if (!(SL_BITS_ABL & 16) && (SL_BITS_UEPI || lane == 0))

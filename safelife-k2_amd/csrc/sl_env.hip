@@ -591,11 +591,18 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     a.draws = cfg->draws;
     a.n_draws = cfg->n_draws;
 
-    const bool fast = cfg->rng_mode == SL_RNG_PHILOX && cfg->kernel != SL_KERNEL_GENERIC &&
-                      fast_shape(st->H, st->W);
-    if (cfg->kernel == SL_KERNEL_FAST && !fast) return SL_ETOOBIG;
+    const bool philox_fast = cfg->rng_mode == SL_RNG_PHILOX && cfg->kernel != SL_KERNEL_GENERIC;
+    const bool fast = philox_fast && fast_shape(st->H, st->W);
+    const bool fast128 = philox_fast && bits128_shape(*st);
+    if (cfg->kernel == SL_KERNEL_FAST && !fast && !fast128) return SL_ETOOBIG;
     bool reset_done = false;
-    if (fast) {
+    if (fast128) {
+        if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
+        int rc = launch_step_bits128(*st, a, actions, cfg->can_toggle_powers,
+                                     cfg->can_toggle_colors, reward, done, info_flags, ep_len,
+                                     ep_reward, s);
+        if (rc) return rc;
+    } else if (fast) {
         FastExtra fx;
         fx.fuse_reset = cfg->auto_reset ? 1 : 0;
         if (pool) fx.pool = *pool;

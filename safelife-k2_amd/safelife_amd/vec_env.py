@@ -123,10 +123,11 @@ class SafeLifeVecEnv:
                                            self.start_board.data_ptr())
         for k, t in self.st_t.items():
             setattr(s, k, t.data_ptr())
-        # bit-plane mirror of board/goals kept by the 64x64 kernel (derived data)
+        # bit-plane mirror of the goals kept by the bit-sliced kernels (derived data):
+        # 64x64 [B, 2, 32, 64] (half 1 = goals), 128x128 [B, 4 bands, 32, 64]
         self.planes_ok = z(B)
-        if (H, W) == (64, 64):
-            self.planes = z(B, 2, 32, 64)
+        if (H, W) in ((64, 64), (128, 128)):
+            self.planes = z(B, H // 32, 32, 64)
             s.planes = self.planes.data_ptr()
             s.planes_ok = self.planes_ok.data_ptr()
         self._state = s

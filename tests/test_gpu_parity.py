@@ -419,6 +419,96 @@ def test_fast_kernel_state_overwrite(torch_dev):
         _compare_state(fast, gen, t)
 
 
+# ------------------------------------------------ 128x128 bit-sliced kernel (C5)
+C5_POOL = os.path.join(GOLDEN, "pools", "c5_navigation_128.npz")
+
+
+def test_fast128_vs_generic(torch_dev):
+    """The 128x128 banded bit-sliced kernel against the per-cell generic kernel on the
+    C5 navigation levels (spawners everywhere, oscillating goals in level 3): rewards,
+    done, flags, observations every step, all state every few steps, across resets."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    pool = LevelPool.load(C5_POOL)
+    rng = np.random.RandomState(17)
+    B, T = 160, 90
+    kw = dict(time_limit=35, view_shape=(33, 33), output_channels=None, penalty_coef=0.7,
+              min_performance=0.01, rng="philox", seed=77, level_order="random",
+              augment_roll=True)
+    fast = SafeLifeVecEnv(pool, B, "cuda:0", kernel="fast", **kw)
+    gen = SafeLifeVecEnv(pool, B, "cuda:0", kernel="generic", **kw)
+    o1, o2 = fast.reset(), gen.reset()
+    assert torch.equal(o1, o2)
+    for t in range(T):
+        a = torch.from_numpy(rng.choice(9, size=B, p=[.05] + [.1] * 4 + [.1375] * 4)
+                             .astype(np.int32)).to(dev)
+        o1, r1, d1, _ = fast.step(a)
+        o2, r2, d2, _ = gen.step(a)
+        assert torch.equal(r1, r2), (t, (r1 - r2).abs().max().item())
+        assert torch.equal(d1, d2), t
+        assert torch.equal(fast.flags, gen.flags), t
+        assert torch.equal(o1, o2), t
+        if t % 7 == 0 or t == T - 1:
+            _compare_state(fast, gen, t)
+
+
+def test_fast128_vs_oracle(torch_dev):
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    levels = _levels_from_pool(C5_POOL)
+    B, T = 6, 24
+    kw = dict(time_limit=1000, view_shape=(15, 15), output_channels=None, penalty_coef=1.0,
+              min_performance=0.01)
+    venv = SafeLifeVecEnv(LevelPool.load(C5_POOL), B, "cuda:0", rng="philox", seed=3,
+                          kernel="fast", **kw)
+    oenvs = _oracle_envs(levels, B, rng="philox", seed=3, **kw)
+    venv.reset()
+    for e in range(B):
+        oenvs[e].reset()
+    rng = np.random.RandomState(4)
+    for t in range(T):
+        acts = rng.randint(0, 9, size=B).astype(np.int32)
+        _, vr, vd, _ = venv.step(torch.from_numpy(acts).to(dev))
+        vr, vd = vr.cpu().numpy(), vd.cpu().numpy()
+        vb, vg = venv.board.cpu().numpy(), venv.goals.cpu().numpy()
+        for e in range(B):
+            _, r, dn, _ = oenvs[e].step(int(acts[e]))
+            assert vr[e] == r, (t, e, vr[e], r)
+            assert bool(vd[e]) == dn, (t, e)
+            assert np.array_equal(vb[e], oenvs[e].board), (t, e)
+            assert np.array_equal(vg[e], oenvs[e].goals), (t, e)
+
+
+def test_fast128_state_overwrite(torch_dev):
+    """set_state mid-run invalidates the 128x128 kernel's goals mirror."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    B, T = 64, 30
+    kw = dict(time_limit=25, view_shape=(15, 15), output_channels=None, penalty_coef=1.0,
+              min_performance=0.01, rng="philox", seed=5, level_order="random",
+              augment_roll=True)
+    fast = SafeLifeVecEnv(LevelPool.load(C5_POOL), B, "cuda:0", kernel="fast", **kw)
+    gen = SafeLifeVecEnv(LevelPool.load(C5_POOL), B, "cuda:0", kernel="generic", **kw)
+    fast.reset()
+    gen.reset()
+    rng = np.random.RandomState(8)
+    for t in range(T):
+        a = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+        if t == 12:
+            perm = np.roll(np.arange(B), 3)
+            bd, gl, sb = (x.cpu().numpy()[perm] for x in (fast.board, fast.goals,
+                                                          fast.start_board))
+            sc = {k: v.cpu().numpy()[perm] for k, v in fast.st_t.items()
+                  if k != "start_roll"}
+            fast.set_state(bd, gl, sb, **sc)
+            gen.set_state(bd, gl, sb, **sc)
+        _, r1, d1, _ = fast.step(a)
+        _, r2, d2, _ = gen.step(a)
+        assert torch.equal(r1, r2), t
+        assert torch.equal(d1, d2), t
+        _compare_state(fast, gen, t)
+
+
 # ------------------------------------------------------- side-effect densities (A15)
 def test_side_effect_densities_reference_fixture(torch_dev):
     """sl_side_effect_densities in replay mode reproduces the reference's density maps
