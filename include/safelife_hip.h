@@ -199,13 +199,18 @@ typedef struct sl_level_pool {
     const float *spawn_prob;
     const double *min_performance;  /* the level's own value (used for the
                                        reset-time exit colour only)           */
-    uint64_t *board_planes;   /* [K,16,W] or NULL (64x64 pools): bit planes of
-                                 each board, element [k][p][x] has bit y = bit p
-                                 of board[k][y][x] (sl_level_pool_prepare)      */
+    uint64_t *board_planes;   /* bit planes of the pool boards, or NULL
+                                 (sl_level_pool_prepare; the bit-sliced kernels'
+                                 start-board source):
+                                 64x64 pools: uint64 [K,16,W], element [k][p][x]
+                                 bit y = bit p of board[k][y][x];
+                                 128x128 pools: uint32 [K,16,4,W] (8*K*16*W
+                                 bytes), element [k][p][q][x] bit r = bit p of
+                                 board[k][32q + r][x]                          */
 } sl_level_pool;
 
-/* Fill pool->board_planes (caller-allocated, dev uint64 [K,16,W]; H must be 64)
- * from pool->board.  Derived data only; the reference keeps levels as npz
+/* Fill pool->board_planes (caller-allocated, dev, layout above; H must be 64 or
+ * 128) from pool->board.  Derived data only; the reference keeps levels as npz
  * (safelife_game.py:184-194). */
 int sl_level_pool_prepare(sl_level_pool *pool, void *stream);
 

@@ -80,6 +80,11 @@ struct Geo64 {
     __device__ __forceinline__ u32 cell(int y, int w) const {
         return (u32)((32 * (lane & 1) + y) * N + 2 * (lane >> 1) + w);
     }
+    // spawners are rare on these boards: per-lane draws, no LDS list
+    __device__ __forceinline__ void draws(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
+                                          u32 tensor) const {
+        lane_draws(*this, elig, sp, sc, tensor);
+    }
 };
 
 // ---------------------------------------------------------------- LDS staging

@@ -377,16 +377,27 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
     }
 }
 
-// pool->board_planes[k][p][x] bit y = bit p of pool->board[k][y][x]  (H == 64)
+// pool->board_planes (H == 64): [k][p][x] bit y = bit p of pool->board[k][y][x];
+// (H == 128): 32-bit words [k][p][q][x] bit r = bit p of pool->board[k][32q + r][x]
 __global__ void __launch_bounds__(NT) k_pool_planes(sl_level_pool pool) {
-    const int64_t n = (int64_t)pool.K * 16 * pool.W;
+    const int nq = pool.H / 32;            // 32-row words per column (2 or 4)
+    const int64_t n = (int64_t)pool.K * 16 * nq * pool.W;
     for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-        const int64_t k = i / (16 * pool.W);
-        const int r = (int)(i - k * 16 * pool.W), p = r / pool.W, x = r - p * pool.W;
-        const uint16_t *bd = pool.board + k * 64 * pool.W + x;
-        uint64_t v = 0;
-        for (int y = 0; y < 64; y++) v |= (uint64_t)((bd[y * pool.W] >> p) & 1u) << y;
-        pool.board_planes[i] = v;
+        const int64_t k = i / (16 * nq * pool.W);
+        int r = (int)(i - k * 16 * nq * pool.W);
+        const int p = r / (nq * pool.W);
+        r -= p * nq * pool.W;
+        const int q = r / pool.W, x = r - q * pool.W;
+        const uint16_t *bd = pool.board + (k * pool.H + 32 * q) * pool.W + x;
+        uint32_t v = 0;
+        for (int y = 0; y < 32; y++) v |= (uint32_t)((bd[y * pool.W] >> p) & 1u) << y;
+        if (pool.H == 64) {
+            uint32_t *w = reinterpret_cast<uint32_t *>(pool.board_planes) +
+                          2 * ((k * 16 + p) * pool.W + x) + q;
+            *w = v;
+        } else {
+            reinterpret_cast<uint32_t *>(pool.board_planes)[i] = v;
+        }
     }
 }
 
@@ -545,10 +556,10 @@ extern "C" int sl_event_elapsed_ms(void *begin, void *end, float *ms) {
 }
 
 extern "C" int sl_level_pool_prepare(sl_level_pool *pool, void *stream) {
-    if (!pool || pool->K <= 0 || pool->H != 64 || pool->W < 2 || !pool->board ||
-        !pool->board_planes)
+    if (!pool || pool->K <= 0 || (pool->H != 64 && pool->H != 128) || pool->W < 2 ||
+        !pool->board || !pool->board_planes)
         return SL_EINVAL;
-    const int64_t n = (int64_t)pool->K * 16 * pool->W;
+    const int64_t n = (int64_t)pool->K * 16 * (pool->H / 32) * pool->W;
     const unsigned grid = (unsigned)std::min<int64_t>((n + NT - 1) / NT, 4096);
     hipLaunchKernelGGL(k_pool_planes, dim3(grid), dim3(NT), 0, (hipStream_t)stream, *pool);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
@@ -598,7 +609,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     bool reset_done = false;
     if (fast128) {
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
-        int rc = launch_step_bits128(*st, a, actions, cfg->can_toggle_powers,
+        int rc = launch_step_bits128(*st, a, pool, actions, cfg->can_toggle_powers,
                                      cfg->can_toggle_colors, reward, done, info_flags, ep_len,
                                      ep_reward, s);
         if (rc) return rc;

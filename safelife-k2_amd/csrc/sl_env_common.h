@@ -250,9 +250,9 @@ int launch_step_fast(const sl_env_state &st, const StepArgs &a, const FastExtra 
 bool launch_fast_fuses_reset(const sl_env_state &st, const FastExtra &fx);
 // bit-sliced 128x128 kernel (sl_bits128.hip); needs the goals mirror (st.planes)
 bool bits128_shape(const sl_env_state &st);
-int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const int32_t *actions,
-                        int ctp, int ctc, double *reward, uint8_t *done, uint8_t *flags,
-                        int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
+int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const sl_level_pool *pool,
+                        const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
+                        uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
 // bit-sliced 64x64 kernel (sl_bits.hip)
 int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,

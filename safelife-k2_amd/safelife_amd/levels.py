@@ -115,10 +115,11 @@ class LevelPool:
         for k in ("board", "goals", "agent_x", "agent_y", "orientation", "spawn_prob",
                   "min_performance"):
             setattr(s, k, t[k].data_ptr())
-        if self.H == 64:
-            # derived: per-level bit planes (the 64x64 kernel's start-board source)
-            t["board_planes"] = torch.empty((self.K, 16, self.W), dtype=torch.int64,
-                                            device=device)
+        if self.H in (64, 128):
+            # derived: per-level bit planes (the bit-sliced kernels' start-board source),
+            # uint64 [K,16,W] for 64 rows, uint32 [K,16,4,W] for 128
+            t["board_planes"] = torch.empty((self.K, 16, self.H // 32, self.W),
+                                            dtype=torch.int32, device=device)
             s.board_planes = t["board_planes"].data_ptr()
             L = _lib.lib()
             _lib.check(L.sl_level_pool_prepare(ctypes.byref(s), _lib.stream_ptr(device)),
