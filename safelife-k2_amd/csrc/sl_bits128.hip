@@ -26,7 +26,8 @@
 //    0 against the board in HBM before any band is stored; its cell edits are
 //    broadcast and written into the band planes and halo rows before the rule;
 //  * exits are rewritten by the epilogue after the band stores have completed.
-// Finished envs are reset by the generic follow-up kernel (k_env_reset_scan).
+// Finished envs are queued and reset by a follow-up kernel (k_env_reset_list_wide,
+// one 1024-thread block per env).
 #include "sl_bits.h"
 
 using namespace sl;
@@ -195,7 +196,7 @@ __device__ __forceinline__ void pool_start(const u32 *__restrict__ pp, int t, in
 }
 
 __global__ void __launch_bounds__(64, SL_B128_MINW)
-k_env_step_bits128(sl_env_state st, StepArgs a, sl_level_pool pool,
+k_env_step_bits128(sl_env_state st, StepArgs a, FastExtra fx,
                    const int32_t *__restrict__ actions, int ctp,
                    int ctc, double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
                    uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
@@ -316,6 +317,7 @@ k_env_step_bits128(sl_env_state st, StepArgs a, sl_level_pool pool,
     // ---- board, band by band: rule, scores, changed rows back.  The start board
     // comes from the level pool's planes when the env was reset from the pool
     // (start_roll = (dy << 16) | dx), else from HBM (written by the caller).
+    const sl_level_pool &pool = fx.pool;
     const int roll = (!SL_B128_NOPOOL && pool.board_planes && pool.K > 0 && pool.H == N &&
                       pool.W == N &&
                       st.start_roll) ? rec(V, R_ROLL) : -1;
@@ -399,9 +401,16 @@ k_env_step_bits128(sl_env_state st, StepArgs a, sl_level_pool pool,
     const int possible = wave_total(pos), side_total = wave_total(side);
     wait_vm();              // row stores land before the epilogue rewrites the exits
     TM_SET(9);
-    if (lane == 0)
-        epilogue_core(st, a, b, fl, act_reward, points, score, possible, side_total, reward_out,
-                      done_out, flags_out, ep_len_out, ep_rew_out);
+    if (lane == 0) {
+        const bool reset = epilogue_core(st, a, b, fl, act_reward, points, score, possible,
+                                         side_total, reward_out, done_out, flags_out, ep_len_out,
+                                         ep_rew_out);
+        if (fx.fuse_reset && reset) {   // queued for k_env_reset_list_wide
+            int64_t *cnt = fx.scratch + 8 * st.B + 2 + (a.step & 1);
+            const int i = (int)atomicAdd((unsigned long long *)cnt, 1ull);
+            reinterpret_cast<int32_t *>(fx.scratch + 2 * st.B)[i] = (int32_t)b;
+        }
+    }
 #if SL_B128_TIMING
     TM_SET(10);
     if ((b & 63) == 0 && lane == 0)
@@ -424,14 +433,16 @@ bool bits128_shape(const sl_env_state &st) {
     return st.H == N && st.W == N && st.planes && st.planes_ok;
 }
 
-int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const sl_level_pool *pool,
+int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                         const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                         uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (!bits128_shape(st)) return SL_ETOOBIG;
-    const sl_level_pool pl = pool ? *pool : sl_level_pool{};
-    hipLaunchKernelGGL(k_env_step_bits128, dim3((unsigned)st.B), dim3(64), 0, s, st, a, pl, actions,
-                       ctp, ctc, reward, done, flags, ep_len, ep_rew);
-    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+    hipLaunchKernelGGL(k_env_step_bits128, dim3((unsigned)st.B), dim3(64), 0, s, st, a, fx,
+                       actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+    if (hipGetLastError() != hipSuccess) return SL_EHIP;
+    if (fx.fuse_reset && fx.pool.K > 0)
+        return launch_reset_list_wide(st, fx.pool, fx.ra, fx.scratch, a.step, s);
+    return SL_OK;
 }
 
 }  // namespace sl

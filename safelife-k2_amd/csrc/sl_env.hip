@@ -377,6 +377,139 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
     }
 }
 
+// The same reset by a 1024-thread block, for the envs a step kernel queued (the
+// 128x128 kernel).  The exit cells are appended to an LDS list by atomics and put
+// into np.nonzero order afterwards, so the load pass has no barrier and all of a
+// thread's gathers are in flight together.  A level with more exit cells than the
+// list holds (never seen) is scanned in order by one thread.
+constexpr int NTR = 1024;
+constexpr int kExitCap = 64;
+struct WideResetShared {
+    int red[NTR / 64][4];
+    int exl[kExitCap];
+    int nex, ev, idx, dy, dx;
+};
+
+__device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &a,
+                           int64_t b, WideResetShared &sh) {
+    const int H = st.H, W = st.W, hw = H * W;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) {
+        const LevelChoice c = choose_level(pool, a, a.env0 + (uint32_t)b, st.episodes[b], H, W);
+        sh.idx = c.idx;
+        sh.dy = c.dy;
+        sh.dx = c.dx;
+        sh.nex = 0;
+    }
+    __syncthreads();
+    const int idx = sh.idx, dy = sh.dy, dx = sh.dx;
+    const uint16_t *pb = pool.board + (int64_t)idx * hw, *pg = pool.goals + (int64_t)idx * hw;
+
+    int acc[4] = {0, 0, 0, 0};   // points, score (= baseline), possible, spawn flags
+#pragma unroll 4
+    for (int i = tid; i < hw; i += NTR) {
+        const int y = i / W, x = i - y * W;
+        const int src = pymod(y - dy, H) * W + pymod(x - dx, W);
+        const uint32_t vb = pb[src], vg = pg[src];
+        int p, q, r;
+        cell_scores(vb, vg, &p, &q, &r);
+        acc[0] += p;
+        acc[1] += q;
+        acc[2] += r;
+        acc[3] += ((vb & SPAWN) ? 1 : 0) + ((vg & SPAWN) ? 65536 : 0);
+        if (vb & EXIT) {
+            const int k = atomicAdd(&sh.nex, 1);
+            if (k < kExitCap) sh.exl[k] = i;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) acc[k] = wave_sum(acc[k]);
+    if (lane == 0)
+        for (int k = 0; k < 4; k++) sh.red[wid][k] = acc[k];
+    __syncthreads();
+    if (tid == 0) {
+        int t[4] = {0, 0, 0, 0};
+        for (int w = 0; w < NTR / 64; w++)
+            for (int k = 0; k < 4; k++) t[k] += sh.red[w][k];
+        const int spawn_bits = ((t[3] & 0xFFFF) ? 1 : 0) | ((t[3] >> 16) ? 2 : 0);
+        sh.ev = reset_scalars(st, pool, a, b, idx, dy, dx, t[0], t[1], t[2], spawn_bits);
+        const int nex = sh.nex;
+        int16_t *ey = st.exit_y + b * SL_MAX_EXITS, *ex = st.exit_x + b * SL_MAX_EXITS;
+        int n = 0;
+        if (nex <= kExitCap) {           // row-major order = ascending flat index
+            for (int k = 1; k < nex; k++) {
+                const int v = sh.exl[k];
+                int j = k - 1;
+                while (j >= 0 && sh.exl[j] > v) {
+                    sh.exl[j + 1] = sh.exl[j];
+                    j--;
+                }
+                sh.exl[j + 1] = v;
+            }
+            for (; n < nex && n < SL_MAX_EXITS; n++) {
+                ey[n] = (int16_t)(sh.exl[n] / W);
+                ex[n] = (int16_t)(sh.exl[n] % W);
+            }
+        } else {
+            for (int i = 0; i < hw && n < SL_MAX_EXITS; i++) {
+                const int y = i / W, x = i - y * W;
+                if (pb[pymod(y - dy, H) * W + pymod(x - dx, W)] & EXIT) {
+                    ey[n] = (int16_t)y;
+                    ex[n] = (int16_t)x;
+                    n++;
+                }
+            }
+        }
+        for (int e = n; e < SL_MAX_EXITS; e++) {
+            ey[e] = 0;
+            ex[e] = 0;
+        }
+        st.exit_count[b] = nex;
+    }
+    __syncthreads();
+    const uint16_t ev = (uint16_t)sh.ev;
+    uint16_t *gb = st.board + b * hw, *gg = st.goals + b * hw, *gs = st.start_board + b * hw;
+    if ((W & 1) == 0) {                  // cell pairs: one dword store per tensor
+        uint32_t *gb2 = reinterpret_cast<uint32_t *>(gb), *gg2 = reinterpret_cast<uint32_t *>(gg);
+        uint32_t *gs2 = reinterpret_cast<uint32_t *>(gs);
+#pragma unroll 4
+        for (int i = tid; i < (hw >> 1); i += NTR) {
+            const int y = (2 * i) / W, x = 2 * i - y * W;
+            const int sr = pymod(y - dy, H) * W;
+            const int c0 = pymod(x - dx, W), c1 = c0 + 1 == W ? 0 : c0 + 1;
+            const uint32_t b0 = pb[sr + c0], b1 = pb[sr + c1];
+            gs2[i] = b0 | (b1 << 16);
+            gb2[i] = ((b0 & EXIT) ? ev : b0) | ((uint32_t)((b1 & EXIT) ? ev : b1) << 16);
+            gg2[i] = (uint32_t)pg[sr + c0] | ((uint32_t)pg[sr + c1] << 16);
+        }
+    } else {
+        for (int i = tid; i < hw; i += NTR) {
+            const int y = i / W, x = i - y * W;
+            const int src = pymod(y - dy, H) * W + pymod(x - dx, W);
+            const uint16_t vb = pb[src];
+            gs[i] = vb;
+            gb[i] = (vb & EXIT) ? ev : vb;
+            gg[i] = pg[src];
+        }
+    }
+}
+
+// Resets the envs a step kernel queued in the scratch list (sl_env_common.h), one
+// block each; zeroes the other step parity's list length for the next step.
+__global__ void __launch_bounds__(NTR)
+k_env_reset_list_wide(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scratch,
+                      uint32_t step) {
+    __shared__ WideResetShared sh;
+    int64_t *cnt = scratch + 8 * st.B + 2;
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(step + 1) & 1] = 0;
+    const int n = (int)cnt[step & 1];
+    const int32_t *list = reinterpret_cast<const int32_t *>(scratch + 2 * st.B);
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        reset_wide(st, pool, ra, list[i], sh);
+        __syncthreads();
+    }
+}
+
 // pool->board_planes (H == 64): [k][p][x] bit y = bit p of pool->board[k][y][x];
 // (H == 128): 32-bit words [k][p][q][x] bit r = bit p of pool->board[k][32q + r][x]
 __global__ void __launch_bounds__(NT) k_pool_planes(sl_level_pool pool) {
@@ -521,6 +654,16 @@ ResetArgs reset_args(const sl_env_cfg *cfg) {
 
 }  // namespace
 
+namespace sl {
+int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
+                           int64_t *scratch, uint32_t step, hipStream_t s) {
+    const unsigned grid = (unsigned)(st.B < 256 ? st.B : 256);
+    hipLaunchKernelGGL(k_env_reset_list_wide, dim3(grid), dim3(NTR), 0, s, st, pool, ra, scratch,
+                       step);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+}  // namespace sl
+
 extern "C" const char *sl_version(void) { return "safelife-hip 0.1 (gfx950)"; }
 
 extern "C" int sl_device_arch(char *buf, int len) {
@@ -607,19 +750,20 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     const bool fast128 = philox_fast && bits128_shape(*st);
     if (cfg->kernel == SL_KERNEL_FAST && !fast && !fast128) return SL_ETOOBIG;
     bool reset_done = false;
+    FastExtra fx;
+    fx.fuse_reset = cfg->auto_reset ? 1 : 0;
+    if (pool) fx.pool = *pool;
+    else fx.pool = sl_level_pool{};
+    fx.ra = reset_args(cfg);
+    fx.scratch = cfg->scratch;
     if (fast128) {
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
-        int rc = launch_step_bits128(*st, a, pool, actions, cfg->can_toggle_powers,
+        int rc = launch_step_bits128(*st, a, fx, actions, cfg->can_toggle_powers,
                                      cfg->can_toggle_colors, reward, done, info_flags, ep_len,
                                      ep_reward, s);
         if (rc) return rc;
+        reset_done = fx.fuse_reset && fx.pool.K > 0;
     } else if (fast) {
-        FastExtra fx;
-        fx.fuse_reset = cfg->auto_reset ? 1 : 0;
-        if (pool) fx.pool = *pool;
-        else fx.pool = sl_level_pool{};
-        fx.ra = reset_args(cfg);
-        fx.scratch = cfg->scratch;
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
         int rc = launch_step_fast(*st, a, fx, actions, cfg->can_toggle_powers,
                                   cfg->can_toggle_colors, reward, done, info_flags, ep_len,

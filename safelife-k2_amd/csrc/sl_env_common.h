@@ -9,7 +9,7 @@ namespace sl {
 //   [0, 2B)   per-(env, tensor) draw counts      (replay mode)
 //   [2B, 4B)  per-(env, tensor) stream offsets   (replay mode); in Philox mode the
 //             first B int32 slots hold the list of envs to reset after the step
-//             (64x64 kernel)
+//             (64x64 and 128x128 kernels)
 //   [4B, 8B)  per env: action reward, d_points, d_score, d_side of the action's
 //             cell edits (the fast path keeps the scores incrementally)
 //   [8B]      error flags (bit0: draw stream exhausted)
@@ -248,11 +248,17 @@ int launch_step_fast(const sl_env_state &st, const StepArgs &a, const FastExtra 
                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
 // true when the launched fast kernel also performed the auto-resets
 bool launch_fast_fuses_reset(const sl_env_state &st, const FastExtra &fx);
-// bit-sliced 128x128 kernel (sl_bits128.hip); needs the goals mirror (st.planes)
+// bit-sliced 128x128 kernel (sl_bits128.hip); needs the goals mirror (st.planes).
+// With fx.fuse_reset it queues the envs that finished and launches
+// k_env_reset_list_wide for them.
 bool bits128_shape(const sl_env_state &st);
-int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const sl_level_pool *pool,
+int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                         const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                         uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
+// resets of the envs queued in the scratch list for step `step`, one 1024-thread
+// block each (sl_env.hip)
+int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
+                           int64_t *scratch, uint32_t step, hipStream_t s);
 // bit-sliced 64x64 kernel (sl_bits.hip)
 int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
