@@ -32,6 +32,10 @@
  *                       (side_effects.py:59-92,131-139), batched over episodes
  *   sl_level_pool_prepare  derived pool data for the device level pool
  *                       (levels as loaded by safelife_game.py:184-212)
+ *   sl_sample_actions   np.random.choice(len(policy), p=policy) per env in
+ *                       PPO.run_agents (training/ppo.py:440)
+ *   sl_gae              returns + advantages of PPO.gen_training_batch
+ *                       (training/ppo.py:487-503)
  */
 #ifndef SAFELIFE_HIP_H
 #define SAFELIFE_HIP_H
@@ -62,6 +66,9 @@ extern "C" {
 #define SL_OBS_PACKED 1     /* uint16 [B, vh, vw]           (output_channels=None) */
 #define SL_OBS_CHANNELS 2   /* uint16 [B, vh, vw, nch]      (output_channels=(...)) */
 #define SL_OBS_CHANNELS_U8 3 /* uint8 [B, vh, vw, nch]      (same values, 1 byte)  */
+#define SL_OBS_CHANNELS_F32 4 /* float [B, vh, vw, nch]     0.0 / 1.0: the policy's
+                                 layer0 (training/safelife_ppo.py:147-152)        */
+#define SL_OBS_CHANNELS_BF16 5 /* bfloat16 [B, vh, vw, nch] 0.0 / 1.0             */
 
 /* Library / device info. */
 const char *sl_version(void);
@@ -266,12 +273,44 @@ int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const uint8_t *mas
 /*
  * Observations centred on each agent.
  *   obs_mode SL_OBS_PACKED: out uint16 [B,vh,vw]; SL_OBS_CHANNELS: uint16
- *   [B,vh,vw,nch] with channel k = bit channels[k]; SL_OBS_CHANNELS_U8: uint8.
+ *   [B,vh,vw,nch] with channel k = bit channels[k]; SL_OBS_CHANNELS_U8: uint8;
+ *   SL_OBS_CHANNELS_F32 / _BF16: the same bits as 0.0 / 1.0 floats.
  *   channels: host int array [nch] (<= 16) -- copied into kernel arguments.
  */
 int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_white_goals,
                int obs_mode, const int32_t *channels, int nch, void *out,
                void *stream);
+
+/* ------------------------------------------------------- PPO caller -- */
+
+/*
+ * actions[b] = np.random.choice(A, p=probs[b]) (numpy's legacy RandomState.choice:
+ * p taken as float64, cdf = cumsum(p) / cdf[-1], index = #{k : cdf[k] <= u}).
+ *   probs       dev float32 (probs_f64 = 0) or float64 [B, ld], first A used
+ *   rng_mode    SL_RNG_STREAM: u = uniforms[b] (dev double [B], e.g. the global
+ *               numpy stream); SL_RNG_PHILOX: u = philox(seed; 0, env0 + b, step, 2)
+ *   atol        numpy's tolerance on |sum(p) - 1| (sqrt(eps) of float64, or of
+ *               the probabilities' dtype when larger)
+ *   err         dev uint8 [B] or NULL: bit0 some p < 0, bit1 |kahan_sum(p) - 1|
+ *               > atol -- the ValueErrors numpy raises; the caller raises them
+ */
+int sl_sample_actions(const void *probs, int probs_f64, int64_t B, int A, int64_t ld,
+                      int rng_mode, const double *uniforms, uint64_t seed, uint32_t env0,
+                      uint32_t step, double atol, int32_t *actions, uint8_t *err,
+                      void *stream);
+
+/*
+ * Discounted returns and GAE advantages over a rollout of T steps x N envs with G
+ * discount factors, in the reference's dtypes and evaluation order:
+ *   rewards      dev double [T, N]   (clipped to +-reward_clip when > 0)
+ *   end_episode  dev uint8 [T, N]
+ *   values       dev float [T+1, N, G]
+ *   gamma, lmda  dev float [G]       (lmda = the reference's lmda * gamma, float32)
+ *   returns, advantages  dev double [T, N, G]
+ */
+int sl_gae(const double *rewards, const uint8_t *end_episode, const float *values,
+           const float *gamma, const float *lmda, int G, int T, int64_t N,
+           double reward_clip, double *returns, double *advantages, void *stream);
 
 #ifdef __cplusplus
 }

@@ -515,3 +515,61 @@ class OracleEnv:
             obs = self.reset()
         self.step_counter += 1
         return obs, float(reward), done, info
+
+
+# ---------------------------------------------------------------------------
+# The PPO caller's per-step arithmetic (training/ppo.py), restated in numpy.
+# ---------------------------------------------------------------------------
+def choice_atol(p_dtype):
+    """The tolerance numpy's legacy RandomState.choice allows on sum(p) - 1."""
+    atol = np.sqrt(np.finfo(np.float64).eps)
+    if np.issubdtype(p_dtype, np.floating):
+        atol = max(atol, np.sqrt(np.finfo(p_dtype).eps))
+    return float(atol)
+
+
+def sample_action(p, u):
+    """``np.random.choice(len(p), p=p)`` given its uniform draw ``u`` (ppo.py:440).
+
+    Restates numpy's legacy ``RandomState.choice`` for a 1-d ``p`` and ``size=None``:
+    p as float64, cdf = cumsum(p) / cdf[-1], index = cdf.searchsorted(u, 'right').
+    Returns (index, err) with err bit0 = some p < 0, bit1 = |kahan_sum(p) - 1| > atol
+    (the two ValueErrors numpy raises).  Pinned against RandomState.choice itself by
+    tests/test_rollout_cpu.py."""
+    atol = choice_atol(np.asarray(p).dtype)
+    pd = np.asarray(p, dtype=np.float64)
+    s, c = pd[0], 0.0
+    for v in pd[1:]:
+        y = v - c
+        t = s + y
+        c = (t - s) - y
+        s = t
+    err = (1 if np.any(pd < 0) else 0) | (2 if abs(s - 1.0) > atol else 0)
+    cdf = pd.cumsum()
+    cdf /= cdf[-1]
+    return int(cdf.searchsorted(u, side="right")), err
+
+
+def gae(rewards, end_episode, values, gamma=(0.99,), lmda=0.95, reward_clip=0.0):
+    """Discounted returns and GAE advantages of ``PPO.gen_training_batch``
+    (training/ppo.py:487-503), with the reference's dtypes: rewards float64 [T,N],
+    end_episode bool [T,N], values float32 [T+1,N,G], gamma float32 [G]
+    (ppo.py:116-117).  Returns (returns, advantages), float64 [T,N,G]."""
+    rewards = np.asarray(rewards, dtype=np.float64)
+    end_episode = np.asarray(end_episode, dtype=bool)
+    values = np.asarray(values, dtype=np.float32)
+    gamma = np.asarray(gamma, dtype=np.float32)
+    steps_per_env = rewards.shape[0]
+    if reward_clip > 0:
+        rewards = np.clip(rewards, -reward_clip, reward_clip)
+    reward_mask = ~end_episode[..., np.newaxis]
+    rewards = rewards[..., np.newaxis]
+    lmda = lmda * gamma
+    n_gamma = len(gamma)
+    advantages = rewards + gamma * reward_mask * values[1:] - values[:-1]
+    returns = np.broadcast_to(rewards, rewards.shape[:-1] + (n_gamma,)).copy()
+    returns[-1] += reward_mask[-1] * gamma * values[-1]
+    for i in range(steps_per_env - 2, -1, -1):
+        returns[i] += gamma * reward_mask[i] * returns[i + 1]
+        advantages[i] += lmda * reward_mask[i] * advantages[i + 1]
+    return returns, advantages

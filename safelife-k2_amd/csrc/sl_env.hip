@@ -582,6 +582,19 @@ __device__ __forceinline__ uint16_t obs_value(uint32_t bv, uint32_t gv, int remo
     return (uint16_t)((bv + (g << 3)) & 0xFFFFu);
 }
 
+// channel k of cell i = bit a.ch[k] of view[i], stored as the pattern 0 / `one` of an
+// element type of T's width (0/1 integers, or 0.0/1.0 as float32 / bfloat16 -- the
+// policy's layer0, training/safelife_ppo.py:147-152, without a separate cast pass)
+template <typename T>
+__device__ __forceinline__ void store_channels(void *out, int64_t b, const uint16_t *view, int nv,
+                                               const ObsArgs &a, uint32_t one) {
+    T *o = (T *)out + b * (int64_t)nv * a.nch;
+    for (int j = threadIdx.x; j < nv * a.nch; j += NT) {
+        const int i = j / a.nch, k = j - i * a.nch;
+        o[j] = (T)(((view[i] >> a.ch[k]) & 1u) ? one : 0u);
+    }
+}
+
 __global__ void __launch_bounds__(NT)
 k_env_obs(sl_env_state st, ObsArgs a, void *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint16_t view[];
@@ -612,17 +625,13 @@ k_env_obs(sl_env_state st, ObsArgs a, void *__restrict__ out) {
         uint16_t *o = (uint16_t *)out + b * nv;
         for (int i = threadIdx.x; i < nv; i += NT) o[i] = view[i];
     } else if (a.mode == SL_OBS_CHANNELS) {
-        uint16_t *o = (uint16_t *)out + b * (int64_t)nv * a.nch;
-        for (int j = threadIdx.x; j < nv * a.nch; j += NT) {
-            const int i = j / a.nch, k = j - i * a.nch;
-            o[j] = (uint16_t)((view[i] >> a.ch[k]) & 1u);
-        }
+        store_channels<uint16_t>(out, b, view, nv, a, 1u);
+    } else if (a.mode == SL_OBS_CHANNELS_U8) {
+        store_channels<uint8_t>(out, b, view, nv, a, 1u);
+    } else if (a.mode == SL_OBS_CHANNELS_F32) {
+        store_channels<uint32_t>(out, b, view, nv, a, 0x3F800000u);    // 1.0f
     } else {
-        uint8_t *o = (uint8_t *)out + b * (int64_t)nv * a.nch;
-        for (int j = threadIdx.x; j < nv * a.nch; j += NT) {
-            const int i = j / a.nch, k = j - i * a.nch;
-            o[j] = (uint8_t)((view[i] >> a.ch[k]) & 1u);
-        }
+        store_channels<uint16_t>(out, b, view, nv, a, 0x3F80u);        // 1.0 bf16
     }
 }
 
@@ -812,8 +821,7 @@ extern "C" int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_whi
                           void *stream) {
     if (!state_ok(st) || vh < 1 || vw < 1 || (int64_t)vh * vw > kMaxCells || !out)
         return SL_EINVAL;
-    if (obs_mode != SL_OBS_PACKED && obs_mode != SL_OBS_CHANNELS && obs_mode != SL_OBS_CHANNELS_U8)
-        return SL_EINVAL;
+    if (obs_mode < SL_OBS_PACKED || obs_mode > SL_OBS_CHANNELS_BF16) return SL_EINVAL;
     ObsArgs a;
     a.vh = vh;
     a.vw = vw;

@@ -18,6 +18,7 @@ SL_KERNEL_AUTO, SL_KERNEL_GENERIC, SL_KERNEL_FAST = 0, 1, 2
 SL_MAX_EXITS = 8
 SL_BONUS_PERIOD_MAX = 16
 SL_OBS_NONE, SL_OBS_PACKED, SL_OBS_CHANNELS, SL_OBS_CHANNELS_U8 = 0, 1, 2, 3
+SL_OBS_CHANNELS_F32, SL_OBS_CHANNELS_BF16 = 4, 5
 
 _ERRORS = {SL_EINVAL: "invalid argument / shape", SL_EHIP: "HIP launch error",
            SL_ETOOBIG: "board too large for this kernel"}
@@ -102,12 +103,16 @@ def lib():
                                            ctypes.c_int, vp, vp, vp, vp, vp, vp, i64, vp]
     L.sl_env_obs.argtypes = [ctypes.POINTER(EnvState), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                              ctypes.c_int, vp, ctypes.c_int, vp, vp]
+    L.sl_sample_actions.argtypes = [vp, ctypes.c_int, i64, ctypes.c_int, i64, ctypes.c_int, vp,
+                                    u64, u32, u32, f64, vp, vp, vp]
+    L.sl_gae.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, i64, f64, vp, vp, vp]
     L.sl_event_create.argtypes = [ctypes.POINTER(vp)]
     L.sl_event_destroy.argtypes = [vp]
     L.sl_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(f32)]
     for name in ("sl_event_create", "sl_event_destroy", "sl_event_elapsed_ms", "sl_device_arch", "sl_advance", "sl_count_eligible", "sl_exclusive_scan_i64",
                  "sl_env_step", "sl_env_reset", "sl_env_obs", "sl_level_pool_prepare",
-                 "sl_side_effect_workspace", "sl_side_effect_densities"):
+                 "sl_side_effect_workspace", "sl_side_effect_densities",
+                 "sl_sample_actions", "sl_gae"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

@@ -145,12 +145,14 @@ class SafeLifeVecEnv:
             self.obs = z(B, vh, vw, dt=torch.uint16)
         else:
             nch = len(self.output_channels)
-            if obs_dtype == "uint8":
-                self.obs_mode = _lib.SL_OBS_CHANNELS_U8
-                self.obs = z(B, vh, vw, nch, dt=torch.uint8)
-            else:
-                self.obs_mode = _lib.SL_OBS_CHANNELS
-                self.obs = z(B, vh, vw, nch, dt=torch.uint16)
+            modes = {"uint16": (_lib.SL_OBS_CHANNELS, torch.uint16),
+                     "uint8": (_lib.SL_OBS_CHANNELS_U8, torch.uint8),
+                     "float32": (_lib.SL_OBS_CHANNELS_F32, torch.float32),
+                     "bfloat16": (_lib.SL_OBS_CHANNELS_BF16, torch.bfloat16)}
+            if obs_dtype not in modes:
+                raise ValueError("obs_dtype must be one of %s" % sorted(modes))
+            self.obs_mode, dt = modes[obs_dtype]
+            self.obs = z(B, vh, vw, nch, dt=dt)
             self._channels = (ctypes.c_int32 * nch)(*self.output_channels)
         self._pool_dev = self.pool.to_device(self.device)
         self._cfg = _lib.EnvCfg()
@@ -230,15 +232,23 @@ class SafeLifeVecEnv:
             self.torch.count_nonzero(m).item())
         return self.observe() if self.compute_obs else None
 
-    def observe(self):
+    def observe(self, out=None):
+        """Write the observations into `out` (a tensor shaped and typed like
+        self.obs, e.g. one slot of a rollout buffer) or self.obs; returns it."""
         L = _lib.lib()
         vh, vw = self.view_shape
         ch = self._channels if self.obs_mode != _lib.SL_OBS_PACKED else None
         nch = len(self.output_channels) if self.output_channels else 0
+        if out is None:
+            out = self.obs
+        elif (out.shape != self.obs.shape or out.dtype != self.obs.dtype
+              or out.device != self.device or not out.is_contiguous()):
+            raise ValueError("obs out must be a contiguous %s %s tensor on %s"
+                             % (tuple(self.obs.shape), self.obs.dtype, self.device))
         _lib.check(L.sl_env_obs(ctypes.byref(self._state), vh, vw, int(self.remove_white_goals),
-                                self.obs_mode, ch, nch, self.obs.data_ptr(),
+                                self.obs_mode, ch, nch, out.data_ptr(),
                                 _lib.stream_ptr(self.device)), "sl_env_obs")
-        return self.obs
+        return out
 
     def step(self, actions):
         """One env-step for every env.  `actions`: int [B] (torch or numpy), 0..8.
@@ -250,7 +260,13 @@ class SafeLifeVecEnv:
         self.step_async(actions)
         return self.step_wait()
 
-    def step_async(self, actions):
+    def step_async(self, actions, reward_out=None, done_out=None, obs_out=None,
+                   flags_out=None, ep_len_out=None, ep_rew_out=None):
+        """Launch one env-step (stream-ordered, no host sync).  reward_out (float64
+        [B]), done_out / flags_out (uint8 [B]), ep_len_out / ep_rew_out (int32 [B])
+        and obs_out (like self.obs) optionally redirect the outputs, e.g. into one
+        time slot of a rollout buffer; the env's own tensors are then left as they
+        were."""
         torch = self.torch
         a = torch.as_tensor(actions)
         if a.device != self.device or a.dtype != torch.int32:
@@ -265,14 +281,26 @@ class SafeLifeVecEnv:
         cfg = self._fill_cfg()
         _lib.check(L.sl_env_step(ctypes.byref(self._state), ctypes.byref(self._pool_dev["struct"]),
                                  a.data_ptr(), ctypes.byref(cfg),
-                                 self.reward.data_ptr(), self.done.data_ptr(),
-                                 self.flags.data_ptr(), self.ep_len.data_ptr(),
-                                 self.ep_rew.data_ptr(), _lib.stream_ptr(self.device)),
+                                 self._out(reward_out, self.reward).data_ptr(),
+                                 self._out(done_out, self.done).data_ptr(),
+                                 self._out(flags_out, self.flags).data_ptr(),
+                                 self._out(ep_len_out, self.ep_len).data_ptr(),
+                                 self._out(ep_rew_out, self.ep_rew).data_ptr(),
+                                 _lib.stream_ptr(self.device)),
                    "sl_env_step")
         self._step_index += 1
         self.global_counter.num_steps += self.B
-        if self.compute_obs:
-            self.observe()
+        if self.compute_obs or obs_out is not None:
+            self.observe(obs_out)
+
+    def _out(self, t, default):
+        if t is None:
+            return default
+        if (t.shape != default.shape or t.dtype != default.dtype or t.device != self.device
+                or not t.is_contiguous()):
+            raise ValueError("output must be a contiguous %s %s tensor on %s"
+                             % (tuple(default.shape), default.dtype, self.device))
+        return t
 
     def step_wait(self):
         info = {"times_up": (self.flags & 1) != 0, "game_over": (self.flags & 2) != 0,
