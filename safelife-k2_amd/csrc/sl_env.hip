@@ -635,6 +635,162 @@ k_env_obs(sl_env_state st, ObsArgs a, void *__restrict__ out) {
     }
 }
 
+// ---- wave-per-env observation kernels ---------------------------------------
+// One wave per env, four per workgroup, no block barrier.  Lane l handles the view
+// cells i = l + 64k (flat row-major order).  The cells' board and goals loads are
+// issued eight at a time, all independent, so a wave keeps 16 gathers in flight.
+// Exits are moved onto their clipped position on the view (recenter_view,
+// helper_utils.py:55-72); the targets and values are wave-uniform and computed up
+// front; the last exit in np.nonzero order wins a shared target.
+constexpr int kObsGroup = 8;
+constexpr int kObsMaxCells = 4096;        // view cells handled by the wave kernels
+
+struct ObsWave {
+    const uint16_t *gb, *gg;
+    int ty, tx, ne;
+    int tgt[SL_MAX_EXITS];
+    uint32_t val[SL_MAX_EXITS];
+};
+
+__device__ __forceinline__ void obs_wave_init(const sl_env_state &st, const ObsArgs &a, int64_t b,
+                                              ObsWave &w) {
+    const int H = st.H, W = st.W;
+    const int64_t hw = (int64_t)H * W;
+    w.gb = st.board + b * hw;
+    w.gg = st.goals + b * hw;
+    const int y0 = st.agent_y[b], x0 = st.agent_x[b];
+    w.ty = y0 - a.vh / 2;
+    w.tx = x0 - a.vw / 2;
+    w.ne = min(st.exit_count[b], SL_MAX_EXITS);
+#pragma unroll
+    for (int k = 0; k < SL_MAX_EXITS; k++) {
+        w.tgt[k] = -1;
+        w.val[k] = 0;
+        if (k < w.ne) {
+            const int iy = st.exit_y[b * SL_MAX_EXITS + k], ix = st.exit_x[b * SL_MAX_EXITS + k];
+            int jy = pymod(iy - y0 + H / 2, H) - H / 2;
+            int jx = pymod(ix - x0 + W / 2, W) - W / 2;
+            jy = min(max(jy + a.vh / 2, 0), a.vh - 1);
+            jx = min(max(jx + a.vw / 2, 0), a.vw - 1);
+            w.tgt[k] = jy * a.vw + jx;
+            w.val[k] = obs_value(w.gb[iy * W + ix], w.gg[iy * W + ix], a.remove_white);
+        }
+    }
+}
+
+// values of the cells i = i0 + 64g (g < kObsGroup); (r, c) = position of i0, advanced
+template <class F>
+__device__ __forceinline__ void obs_wave_cells(const sl_env_state &st, const ObsArgs &a,
+                                               const ObsWave &w, int nv, int &i0, int &r, int &c,
+                                               F &&emit) {
+    const int dr = 64 / a.vw, dc = 64 - dr * a.vw;
+    uint32_t bv[kObsGroup], gv[kObsGroup];
+#pragma unroll
+    for (int g = 0; g < kObsGroup; g++) {
+        bv[g] = 0;
+        gv[g] = 0;
+        if (i0 + 64 * g < nv) {
+            const int src = pymod(w.ty + r, st.H) * st.W + pymod(w.tx + c, st.W);
+            bv[g] = w.gb[src];
+            gv[g] = w.gg[src];
+        }
+        r += dr;
+        c += dc;
+        if (c >= a.vw) {
+            c -= a.vw;
+            r++;
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < kObsGroup; g++) {
+        const int i = i0 + 64 * g;
+        if (i < nv) {
+            uint32_t v = obs_value(bv[g], gv[g], a.remove_white);
+#pragma unroll
+            for (int k = 0; k < SL_MAX_EXITS; k++)
+                if (k < w.ne && i == w.tgt[k]) v = w.val[k];
+            emit(i, v);
+        }
+    }
+    i0 += 64 * kObsGroup;
+}
+
+__global__ void __launch_bounds__(256)
+k_env_obs_packed(sl_env_state st, ObsArgs a, uint16_t *__restrict__ out) {
+    const int64_t b = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    if (b >= st.B) return;
+    ObsWave w;
+    obs_wave_init(st, a, b, w);
+    const int nv = a.vh * a.vw;
+    uint16_t *o = out + b * nv;
+    int i0 = lane, r = lane / a.vw, c = lane - (lane / a.vw) * a.vw;
+    while (i0 < nv)
+        obs_wave_cells(st, a, w, nv, i0, r, c, [&](int i, uint32_t v) { o[i] = (uint16_t)v; });
+}
+
+// channel obs: the view is gathered into the wave's LDS buffer, then the env's
+// output bytes [b R, (b+1) R) are written as 16-byte vectors where they cover a
+// whole aligned chunk (R = 32 670 B at 33x33x15 u16 is only 2-byte aligned, so the
+// partial chunks at both ends are written element by element).  ESZ = element
+// bytes; channel k of a cell is bit (chpack >> 4k) & 15 of its value.
+template <int ESZ>
+__global__ void __launch_bounds__(256)
+k_env_obs_channels(sl_env_state st, ObsArgs a, uint64_t chpack, uint32_t one,
+                   uint8_t *__restrict__ out) {
+    __shared__ uint16_t view[4][kObsMaxCells];
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t b = (int64_t)blockIdx.x * 4 + wid;
+    const int lane = threadIdx.x & 63;
+    if (b >= st.B) return;
+    ObsWave w;
+    obs_wave_init(st, a, b, w);
+    const int nv = a.vh * a.vw, nch = a.nch;
+    uint16_t *vw_ = view[wid];
+    int i0 = lane, r = lane / a.vw, c = lane - (lane / a.vw) * a.vw;
+    while (i0 < nv)
+        obs_wave_cells(st, a, w, nv, i0, r, c, [&](int i, uint32_t v) { vw_[i] = (uint16_t)v; });
+    // LDS operations of one wave complete in order: the reads below see the writes
+    __builtin_amdgcn_wave_barrier();
+    const int64_t n_el = (int64_t)nv * nch;                  // elements per env
+    const int64_t base = b * n_el * ESZ;                      // first byte
+    const int64_t end = base + n_el * ESZ;
+    const int64_t c0 = (base + 15) & ~(int64_t)15, c1 = end & ~(int64_t)15;
+    auto elem = [&](int64_t e) -> uint32_t {                  // element e of this env
+        const int cell = (int)(e / nch), k = (int)(e - (int64_t)cell * nch);
+        return ((vw_[cell] >> ((chpack >> (4 * k)) & 15u)) & 1u) ? one : 0u;
+    };
+    // partial chunks at both ends (< 16 bytes each): one element per lane
+    const int head = (int)(((c0 < end ? c0 : end) - base) / ESZ);
+    const int tail = c1 >= c0 ? (int)((end - c1) / ESZ) : 0;
+    int64_t e = -1;
+    if (lane < head) e = lane;
+    else if (lane >= 32 && lane - 32 < tail) e = (c1 - base) / ESZ + (lane - 32);
+    if (e >= 0) {
+        const uint32_t v = elem(e);
+        for (int t = 0; t < ESZ; t++) out[base + e * ESZ + t] = (uint8_t)(v >> (8 * t));
+    }
+    // whole chunks
+    constexpr int NE = 16 / ESZ;
+    for (int64_t q = c0 + 16 * (int64_t)lane; q < c1; q += 16 * 64) {
+        const int64_t e0 = (q - base) / ESZ;
+        int cell = (int)(e0 / nch), k = (int)(e0 - (int64_t)cell * nch);
+        uint32_t v = vw_[cell];
+        uint32_t wv[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int t = 0; t < NE; t++) {
+            const uint32_t bit = (v >> ((chpack >> (4 * k)) & 15u)) & 1u;
+            wv[(t * ESZ) >> 2] |= (bit ? one : 0u) << (((t * ESZ) & 3) * 8);
+            if (++k == nch) {
+                k = 0;
+                ++cell;
+                if (t + 1 < NE) v = vw_[cell];
+            }
+        }
+        *reinterpret_cast<uint4 *>(out + q) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    }
+}
+
 bool set_lds(const void *fn, size_t bytes) {
     if (bytes <= 65536) return true;
     return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) ==
@@ -837,9 +993,30 @@ extern "C" int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_whi
         }
     }
     if (st->B == 0) return SL_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if (obs_mode == SL_OBS_PACKED && vh * vw <= kObsMaxCells) {
+        hipLaunchKernelGGL(k_env_obs_packed, dim3((unsigned)((st->B + 3) / 4)), dim3(256), 0, s,
+                           *st, a, (uint16_t *)out);
+        return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+    }
+    if ((((uintptr_t)out) & 15) == 0 && vh * vw <= kObsMaxCells) {
+        uint64_t chpack = 0;
+        for (int k = 0; k < nch; k++) chpack |= (uint64_t)channels[k] << (4 * k);
+        const uint32_t one = obs_mode == SL_OBS_CHANNELS_F32 ? 0x3F800000u
+                             : obs_mode == SL_OBS_CHANNELS_BF16 ? 0x3F80u : 1u;
+        const dim3 grid((unsigned)((st->B + 3) / 4));
+        uint8_t *o = (uint8_t *)out;
+        if (obs_mode == SL_OBS_CHANNELS_U8)
+            hipLaunchKernelGGL(k_env_obs_channels<1>, grid, dim3(256), 0, s, *st, a, chpack, one, o);
+        else if (obs_mode == SL_OBS_CHANNELS_F32)
+            hipLaunchKernelGGL(k_env_obs_channels<4>, grid, dim3(256), 0, s, *st, a, chpack, one, o);
+        else
+            hipLaunchKernelGGL(k_env_obs_channels<2>, grid, dim3(256), 0, s, *st, a, chpack, one, o);
+        return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+    }
+    // unaligned output: the LDS-staged kernel, one workgroup per env
     const size_t lds = (size_t)vh * vw * sizeof(uint16_t);
     if (!set_lds((const void *)k_env_obs, lds)) return SL_ETOOBIG;
-    hipLaunchKernelGGL(k_env_obs, dim3((unsigned)st->B), dim3(NT), lds, (hipStream_t)stream, *st,
-                       a, out);
+    hipLaunchKernelGGL(k_env_obs, dim3((unsigned)st->B), dim3(NT), lds, s, *st, a, out);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }

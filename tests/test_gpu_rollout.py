@@ -175,3 +175,32 @@ def test_obs_float_channels(torch_dev, dtype):
         oa, *_ = a.step(acts[t])
         of, *_ = f.step(acts[t])
         assert torch.equal(of.float(), oa.float()), t
+
+
+@pytest.mark.parametrize("dtype,ch", [("uint8", tuple(range(15))), ("uint16", (3, 0, 9, 14)),
+                                      ("float32", (8, 1, 2))])
+def test_obs_flat_tail_and_unaligned(torch_dev, dtype, ch):
+    """Channel obs through the 16-byte-chunk kernel with a ragged tail (odd B, odd
+    cell count), against the packed obs; the same into a 1-element-offset buffer
+    (unaligned: the LDS-staged fallback kernel)."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    pool = LevelPool.load(os.path.join(GOLDEN, "pools", "c2_append_still_25.npz"))
+    kw = dict(view_shape=(33, 31), rng="philox", seed=9, time_limit=15)
+    B = 7
+    ep = SafeLifeVecEnv(pool, B, "cuda:0", output_channels=None, **kw)
+    ec = SafeLifeVecEnv(pool, B, "cuda:0", output_channels=ch, obs_dtype=dtype, **kw)
+    ep.reset()
+    ec.reset()
+    n = ec.obs.numel()
+    raw = torch.zeros(n + 1, dtype=ec.obs.dtype, device=dev)
+    un = raw[1:].view(ec.obs.shape)
+    rng = np.random.RandomState(4)
+    for t in range(25):
+        a = torch.from_numpy(rng.randint(0, 9, B).astype(np.int32)).to(dev)
+        p = ep.step(a)[0].cpu().numpy().astype(np.int64)
+        c = ec.step(a)[0].float().cpu().numpy().astype(np.int64)
+        ec.observe(out=un)
+        assert np.array_equal(un.float().cpu().numpy().astype(np.int64), c), t
+        for k, bit in enumerate(ch):
+            assert np.array_equal(c[..., k], (p >> bit) & 1), (t, k)
