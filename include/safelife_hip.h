@@ -247,6 +247,14 @@ typedef struct sl_env_cfg {
     void *ev_begin, *ev_end;        /* optional hipEvent_t pair recorded around
                                        the board-advance kernel (profiling)    */
     int32_t kernel;                 /* SL_KERNEL_*: which advance kernel       */
+    void *obs_out;                  /* dev: sl_env_step also writes every env's
+                                       observation after the step (auto-resets
+                                       included), exactly as sl_env_obs with the
+                                       fields below would; NULL = no observation.
+                                       The 64x64 kernel writes packed views from
+                                       the board it holds on chip (no re-read) */
+    int32_t obs_mode, obs_vh, obs_vw, obs_remove_white, obs_nch;
+    int32_t obs_channels[16];
 } sl_env_cfg;
 
 /*

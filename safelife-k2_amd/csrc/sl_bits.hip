@@ -58,6 +58,9 @@ namespace {
 #ifndef SL_BITS_MINW
 #define SL_BITS_MINW 4       // waves per SIMD the register budget is sized for
 #endif
+#ifndef SL_BITS_MINW_OBS
+#define SL_BITS_MINW_OBS 3   // the same for the instantiation that writes observations
+#endif
 
 constexpr int N = 64;        // rows = columns = lanes
 
@@ -286,6 +289,95 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
     }
 }
 
+// ---------------------------------------------------------------- fused observation
+// SafeLifeEnv.get_obs + recenter_view (safelife_env.py:125-155, helper_utils.py:41-74)
+// of the board the kernel holds on chip, packed (output_channels=None): the same
+// values k_env_obs_packed (sl_env.hip) computes from HBM after the step.  A view
+// cell is board + ((goals & COLORS) << 3) (white goals optionally removed), i.e. the
+// goal colour planes added into planes 12-14.  Board bits 12-14 are unused by every
+// cell type, so (wave-uniform check) the planes are overwritten with the goal colours
+// and ONE transpose yields both the board rows (masked with ~0x7000 per cell for the
+// HBM store) and the view-form rows, which go to the wave's LDS buffer in dma_board's
+// layout; a board with any of those bits set takes a bit-sliced add and two more
+// transposes instead.  Each view cell is then one u16 LDS read.  Envs reset after the
+// step get their view rewritten by k_env_obs_packed_list.
+__device__ __forceinline__ void lds_put_board(lds_u32 *buf, int lane, const u32 D[32]) {
+    const int h = lane & 1, j = lane >> 1;
+    lds_u32 *p = buf + h * 1024 + ((j + 16 * h) & 31);
+#pragma unroll
+    for (int y = 0; y < 32; y++) p[y * 32] = D[y];
+}
+
+__device__ __forceinline__ int lds_cell_idx(int row, int col) {
+    return row * 64 + ((col + 32 * (row >> 5)) & 63);
+}
+
+// exit y (R_EY) or x (R_EX) number e of the record, e = this lane's own index
+__device__ __forceinline__ int lane_exit(const RecFields &fl, int e, int field) {
+    const u32 w = (u32)__builtin_amdgcn_ds_bpermute(4 * (field + (e >> 1)), (int)fl.V);
+    return (int)(int16_t)(w >> (16 * (e & 1)));
+}
+
+__device__ __forceinline__ void write_obs(lds_u32 *buf, const FastExtra &fx, const RecFields &fl,
+                                          int64_t b, int lane) {
+    typedef __attribute__((address_space(3))) uint16_t lds_u16;
+    lds_u16 *cells = reinterpret_cast<lds_u16 *>(buf);
+    int vh = fx.obs_vh, vw = fx.obs_vw;
+    asm volatile("" : "+s"(vh), "+s"(vw));   // keeps the view arithmetic from being hoisted
+    const int nv = vh * vw;
+    const int ty = fl.ay - vh / 2, tx = fl.ax - vw / 2;
+    // exits onto their clipped view positions: lane k < ne handles exit k (values read
+    // before any is moved); the last in np.nonzero order wins a shared target
+    const int ne = min(fl.exit_count(), SL_MAX_EXITS);
+    int tgt = -1;
+    u32 val = 0u;
+    const int iy = lane_exit(fl, lane & 7, R_EY), ix = lane_exit(fl, lane & 7, R_EX);  // all lanes
+    if (lane < ne) {
+        int jy = ((iy - fl.ay + N / 2) & (N - 1)) - N / 2;
+        int jx = ((ix - fl.ax + N / 2) & (N - 1)) - N / 2;
+        jy = min(max(jy + vh / 2, 0), vh - 1);
+        jx = min(max(jx + vw / 2, 0), vw - 1);
+        tgt = jy * vw + jx;
+        val = cells[lds_cell_idx(iy, ix)];
+        // a view no larger than the board shows each board cell at most once: the
+        // exits are moved in the LDS board itself and the gather needs no per-cell test
+        tgt = lds_cell_idx((ty + jy) & (N - 1), (tx + jx) & (N - 1)) | (tgt << 12);
+    }
+    const bool small = vh <= N && vw <= N;
+    if (small)
+        for (int k = 0; k < ne; k++)            // one store instruction per exit, in order
+            if (lane == k) cells[tgt & 4095] = (uint16_t)val;
+    uint16_t *o = fx.obs_out + b * (int64_t)nv;
+    const int dr = 64 / vw, dc = 64 - dr * vw;
+    int r = lane / vw, c = lane - r * vw;
+    if (small) {
+        for (int i = lane; i < nv; i += 64) {
+            o[i] = cells[lds_cell_idx((ty + r) & (N - 1), (tx + c) & (N - 1))];
+            r += dr;
+            c += dc;
+            if (c >= vw) {
+                c -= vw;
+                r++;
+            }
+        }
+    } else {
+        for (int i = lane; i < nv; i += 64) {
+            u32 v = cells[lds_cell_idx((ty + r) & (N - 1), (tx + c) & (N - 1))];
+            for (int k = 0; k < ne; k++)
+                if (i == (__builtin_amdgcn_readlane(tgt, k) >> 12))
+                    v = (u32)__builtin_amdgcn_readlane((int)val, k);
+            o[i] = (uint16_t)v;
+            r += dr;
+            c += dc;
+            if (c >= vw) {
+                c -= vw;
+                r++;
+            }
+        }
+    }
+}
+
+template <bool OBS>
 __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs &a,
                                          const FastExtra &fx, int64_t b, int lane, lds_u32 *buf,
                                          const int32_t *__restrict__ actions, int ctp, int ctc,
@@ -451,13 +543,54 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     const int possible = s2 & 0xFFFF;
     const int side_total = (s2 >> 16) & 0xFFFF;
     const u32 rb = wave_or(cb[0] | cb[1]) | erow;
-    if (rb && !(SL_BITS_ABL & 8)) {
+    if ((rb || OBS) && !(SL_BITS_ABL & 8)) {
         const bool can = can_exit_now(fl.min_performance(), score, fl.baseline(), possible);
 #pragma unroll
         for (int w = 0; w < 2; w++)
             PL(PB, 9, w) = can ? (PL(PB, 9, w) | PL(PB, 8, w)) : (PL(PB, 9, w) & ~PL(PB, 8, w));
-        transpose32(PB);
-        store_pairs<32>(gb, PB, rb);
+        const bool hi = OBS && __ballot((PL(PB, 12, 0) | PL(PB, 13, 0) | PL(PB, 14, 0) |
+                                         PL(PB, 12, 1) | PL(PB, 13, 1) | PL(PB, 14, 1)) != 0u) != 0ull;
+        if (OBS && !hi) {
+            // planes 12-14 := goal colours; the store masks them out again
+#pragma unroll
+            for (int w = 0; w < 2; w++) {
+                const u32 white = fx.obs_rw ? (gcol[0][w] & gcol[1][w] & gcol[2][w]) : 0u;
+#pragma unroll
+                for (int k = 0; k < 3; k++) PL(PB, 12 + k, w) = gcol[k][w] & ~white;
+            }
+            transpose32(PB);
+            if (rb) {
+#pragma unroll
+                for (int y = 0; y < 32; y++)
+                    if ((rb >> y) & 1u) gb[y * 32] = PB[y] & 0x8FFF8FFFu;
+            }
+            lds_put_board(buf, lane, PB);      // the start board in buf has been read out
+        } else {
+            transpose32(PB);
+            if (rb) store_pairs<32>(gb, PB, rb);
+            if (OBS) {      // bits 12-14 in use: add the goal colours bit-sliced
+                transpose32(PB);
+#pragma unroll
+                for (int w = 0; w < 2; w++) {
+                    const u32 white = fx.obs_rw ? (gcol[0][w] & gcol[1][w] & gcol[2][w]) : 0u;
+                    u32 cy = 0u;
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const u32 g = gcol[k][w] & ~white, p = PL(PB, 12 + k, w);
+                        PL(PB, 12 + k, w) = p ^ g ^ cy;
+                        cy = maj(p, g, cy);
+                    }
+                    PL(PB, 15, w) ^= cy;
+                }
+                transpose32(PB);
+                lds_put_board(buf, lane, PB);
+            }
+        }
+    }
+    if (OBS && !(SL_BITS_ABL & 8)) {
+        __builtin_amdgcn_sched_barrier(0);
+        write_obs(buf, fx, fl, b, lane);
+        __builtin_amdgcn_sched_barrier(0);
     }
     int reset = 0;
     if (!(SL_BITS_ABL & 16) && (SL_BITS_UEPI || lane == 0))
@@ -472,7 +605,9 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     }
 }
 
-__global__ void __launch_bounds__(64 * SL_BITS_WPB, SL_BITS_MINW)
+// OBS: also write the packed observation (fx.obs_out)
+template <bool OBS>
+__global__ void __launch_bounds__(64 * SL_BITS_WPB, OBS ? SL_BITS_MINW_OBS : SL_BITS_MINW)
 k_env_step_bits64(sl_env_state st, StepArgs a, FastExtra fx, const int32_t *__restrict__ actions, int ctp,
                   int ctc, double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
                   uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
@@ -483,8 +618,8 @@ k_env_step_bits64(sl_env_state st, StepArgs a, FastExtra fx, const int32_t *__re
     __shared__ __attribute__((aligned(16))) u32 stage[SL_BITS_WPB][N * N / 2];
     if (b >= st.B) return;                 // whole waves only
     lds_u32 *buf = (lds_u32 *)&stage[threadIdx.x >> 6][0];
-    step_env(st, a, fx, b, lane, buf, actions, ctp, ctc, reward_out, done_out, flags_out,
-             ep_len_out, ep_rew_out);
+    step_env<OBS>(st, a, fx, b, lane, buf, actions, ctp, ctc, reward_out, done_out, flags_out,
+                  ep_len_out, ep_rew_out);
 }
 
 // Resets the envs the step kernel queued (one wave per env, grid-stride over the
@@ -509,8 +644,14 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (st.H != N || st.W != N) return SL_ETOOBIG;
     const unsigned grid = (unsigned)((st.B + SL_BITS_WPB - 1) / SL_BITS_WPB);
-    hipLaunchKernelGGL(k_env_step_bits64, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, st, a, fx,
-                       actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+    if (fx.obs_out) {
+        if (fx.obs_vh < 1 || fx.obs_vw < 1 || fx.obs_vh * fx.obs_vw > 4096) return SL_EINVAL;
+        hipLaunchKernelGGL(k_env_step_bits64<true>, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, st,
+                           a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+    } else {
+        hipLaunchKernelGGL(k_env_step_bits64<false>, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, st,
+                           a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+    }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.fuse_reset && fx.pool.K > 0) {
         const unsigned grid = (unsigned)(st.B < 512 ? st.B : 512);

@@ -715,11 +715,8 @@ __device__ __forceinline__ void obs_wave_cells(const sl_env_state &st, const Obs
     i0 += 64 * kObsGroup;
 }
 
-__global__ void __launch_bounds__(256)
-k_env_obs_packed(sl_env_state st, ObsArgs a, uint16_t *__restrict__ out) {
-    const int64_t b = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = threadIdx.x & 63;
-    if (b >= st.B) return;
+__device__ __forceinline__ void obs_packed_wave(const sl_env_state &st, const ObsArgs &a,
+                                                int64_t b, int lane, uint16_t *__restrict__ out) {
     ObsWave w;
     obs_wave_init(st, a, b, w);
     const int nv = a.vh * a.vw;
@@ -727,6 +724,25 @@ k_env_obs_packed(sl_env_state st, ObsArgs a, uint16_t *__restrict__ out) {
     int i0 = lane, r = lane / a.vw, c = lane - (lane / a.vw) * a.vw;
     while (i0 < nv)
         obs_wave_cells(st, a, w, nv, i0, r, c, [&](int i, uint32_t v) { o[i] = (uint16_t)v; });
+}
+
+__global__ void __launch_bounds__(256)
+k_env_obs_packed(sl_env_state st, ObsArgs a, uint16_t *__restrict__ out) {
+    const int64_t b = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (b >= st.B) return;
+    obs_packed_wave(st, a, b, threadIdx.x & 63, out);
+}
+
+// packed obs of the envs the 64x64 step kernel queued for reset, after
+// k_env_reset_list reset them (the step kernel wrote every other env's view)
+__global__ void __launch_bounds__(256)
+k_env_obs_packed_list(sl_env_state st, ObsArgs a, uint16_t *__restrict__ out,
+                      const int64_t *__restrict__ scratch, uint32_t step) {
+    const int n = (int)__builtin_amdgcn_readfirstlane((int)scratch[8 * st.B + 2 + (step & 1)]);
+    const int32_t *list = reinterpret_cast<const int32_t *>(scratch + 2 * st.B);
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (int i = blockIdx.x * 4 + wid; i < n; i += gridDim.x * 4)
+        obs_packed_wave(st, a, __builtin_amdgcn_readfirstlane(list[i]), threadIdx.x & 63, out);
 }
 
 // channel obs: the view is gathered into the wave's LDS buffer, then the env's
@@ -817,9 +833,70 @@ ResetArgs reset_args(const sl_env_cfg *cfg) {
     return r;
 }
 
+int obs_args(int vh, int vw, int remove_white, int mode, const int32_t *channels, int nch,
+             ObsArgs *a) {
+    if (vh < 1 || vw < 1 || (int64_t)vh * vw > kMaxCells) return SL_EINVAL;
+    if (mode < SL_OBS_PACKED || mode > SL_OBS_CHANNELS_BF16) return SL_EINVAL;
+    a->vh = vh;
+    a->vw = vw;
+    a->remove_white = remove_white;
+    a->mode = mode;
+    a->nch = 0;
+    if (mode != SL_OBS_PACKED) {
+        if (!channels || nch < 1 || nch > 16) return SL_EINVAL;
+        a->nch = nch;
+        for (int k = 0; k < nch; k++) {
+            if (channels[k] < 0 || channels[k] > 15) return SL_EINVAL;
+            a->ch[k] = channels[k];
+        }
+    }
+    return SL_OK;
+}
+
+int launch_obs(const sl_env_state &st, const ObsArgs &a, void *out, hipStream_t s) {
+    if (st.B == 0) return SL_OK;
+    const int nv = a.vh * a.vw;
+    if (a.mode == SL_OBS_PACKED && nv <= kObsMaxCells) {
+        hipLaunchKernelGGL(k_env_obs_packed, dim3((unsigned)((st.B + 3) / 4)), dim3(256), 0, s, st,
+                           a, (uint16_t *)out);
+        return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+    }
+    if ((((uintptr_t)out) & 15) == 0 && nv <= kObsMaxCells) {
+        uint64_t chpack = 0;
+        for (int k = 0; k < a.nch; k++) chpack |= (uint64_t)a.ch[k] << (4 * k);
+        const uint32_t one = a.mode == SL_OBS_CHANNELS_F32 ? 0x3F800000u
+                             : a.mode == SL_OBS_CHANNELS_BF16 ? 0x3F80u : 1u;
+        const dim3 grid((unsigned)((st.B + 3) / 4));
+        uint8_t *o = (uint8_t *)out;
+        if (a.mode == SL_OBS_CHANNELS_U8)
+            hipLaunchKernelGGL(k_env_obs_channels<1>, grid, dim3(256), 0, s, st, a, chpack, one, o);
+        else if (a.mode == SL_OBS_CHANNELS_F32)
+            hipLaunchKernelGGL(k_env_obs_channels<4>, grid, dim3(256), 0, s, st, a, chpack, one, o);
+        else
+            hipLaunchKernelGGL(k_env_obs_channels<2>, grid, dim3(256), 0, s, st, a, chpack, one, o);
+        return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+    }
+    // unaligned output or a large view: the LDS-staged kernel, one workgroup per env
+    const size_t lds = (size_t)nv * sizeof(uint16_t);
+    if (!set_lds((const void *)k_env_obs, lds)) return SL_ETOOBIG;
+    hipLaunchKernelGGL(k_env_obs, dim3((unsigned)st.B), dim3(NT), lds, s, st, a, out);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
 }  // namespace
 
 namespace sl {
+int launch_obs_packed_list(const sl_env_state &st, int vh, int vw, int remove_white,
+                           uint16_t *out, const int64_t *scratch, uint32_t step, hipStream_t s) {
+    ObsArgs a;
+    int rc = obs_args(vh, vw, remove_white, SL_OBS_PACKED, nullptr, 0, &a);
+    if (rc) return rc;
+    const unsigned grid = (unsigned)(st.B < 1024 ? (st.B + 3) / 4 : 256);
+    hipLaunchKernelGGL(k_env_obs_packed_list, dim3(grid), dim3(256), 0, s, st, a, out, scratch,
+                       step);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
 int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
                            int64_t *scratch, uint32_t step, hipStream_t s) {
     const unsigned grid = (unsigned)(st.B < 256 ? st.B : 256);
@@ -921,6 +998,19 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     else fx.pool = sl_level_pool{};
     fx.ra = reset_args(cfg);
     fx.scratch = cfg->scratch;
+    // observations: packed views of 64x64 boards come out of the step kernel itself
+    ObsArgs oa;
+    if (cfg->obs_out) {
+        const int rc = obs_args(cfg->obs_vh, cfg->obs_vw, cfg->obs_remove_white, cfg->obs_mode,
+                                cfg->obs_channels, cfg->obs_nch, &oa);
+        if (rc) return rc;
+    }
+    const bool fuse_obs = cfg->obs_out && fast && oa.mode == SL_OBS_PACKED &&
+                          oa.vh * oa.vw <= kObsMaxCells && launch_fast_fuses_obs();
+    fx.obs_out = fuse_obs ? (uint16_t *)cfg->obs_out : nullptr;
+    fx.obs_vh = cfg->obs_vh;
+    fx.obs_vw = cfg->obs_vw;
+    fx.obs_rw = cfg->obs_remove_white;
     if (fast128) {
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
         int rc = launch_step_bits128(*st, a, fx, actions, cfg->can_toggle_powers,
@@ -969,54 +1059,22 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
                            *st, *pool, (const uint8_t *)info_flags, reset_args(cfg));
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
     }
+    if (cfg->obs_out) {
+        if (!fuse_obs || (cfg->auto_reset && !reset_done))
+            return launch_obs(*st, oa, cfg->obs_out, s);
+        if (reset_done)      // views of the envs reset after the step kernel wrote theirs
+            return launch_obs_packed_list(*st, oa.vh, oa.vw, oa.remove_white,
+                                          (uint16_t *)cfg->obs_out, cfg->scratch, cfg->step, s);
+    }
     return SL_OK;
 }
 
 extern "C" int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_white_goals,
                           int obs_mode, const int32_t *channels, int nch, void *out,
                           void *stream) {
-    if (!state_ok(st) || vh < 1 || vw < 1 || (int64_t)vh * vw > kMaxCells || !out)
-        return SL_EINVAL;
-    if (obs_mode < SL_OBS_PACKED || obs_mode > SL_OBS_CHANNELS_BF16) return SL_EINVAL;
+    if (!state_ok(st) || !out) return SL_EINVAL;
     ObsArgs a;
-    a.vh = vh;
-    a.vw = vw;
-    a.remove_white = remove_white_goals;
-    a.mode = obs_mode;
-    a.nch = 0;
-    if (obs_mode != SL_OBS_PACKED) {
-        if (!channels || nch < 1 || nch > 16) return SL_EINVAL;
-        a.nch = nch;
-        for (int k = 0; k < nch; k++) {
-            if (channels[k] < 0 || channels[k] > 15) return SL_EINVAL;
-            a.ch[k] = channels[k];
-        }
-    }
-    if (st->B == 0) return SL_OK;
-    hipStream_t s = (hipStream_t)stream;
-    if (obs_mode == SL_OBS_PACKED && vh * vw <= kObsMaxCells) {
-        hipLaunchKernelGGL(k_env_obs_packed, dim3((unsigned)((st->B + 3) / 4)), dim3(256), 0, s,
-                           *st, a, (uint16_t *)out);
-        return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
-    }
-    if ((((uintptr_t)out) & 15) == 0 && vh * vw <= kObsMaxCells) {
-        uint64_t chpack = 0;
-        for (int k = 0; k < nch; k++) chpack |= (uint64_t)channels[k] << (4 * k);
-        const uint32_t one = obs_mode == SL_OBS_CHANNELS_F32 ? 0x3F800000u
-                             : obs_mode == SL_OBS_CHANNELS_BF16 ? 0x3F80u : 1u;
-        const dim3 grid((unsigned)((st->B + 3) / 4));
-        uint8_t *o = (uint8_t *)out;
-        if (obs_mode == SL_OBS_CHANNELS_U8)
-            hipLaunchKernelGGL(k_env_obs_channels<1>, grid, dim3(256), 0, s, *st, a, chpack, one, o);
-        else if (obs_mode == SL_OBS_CHANNELS_F32)
-            hipLaunchKernelGGL(k_env_obs_channels<4>, grid, dim3(256), 0, s, *st, a, chpack, one, o);
-        else
-            hipLaunchKernelGGL(k_env_obs_channels<2>, grid, dim3(256), 0, s, *st, a, chpack, one, o);
-        return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
-    }
-    // unaligned output: the LDS-staged kernel, one workgroup per env
-    const size_t lds = (size_t)vh * vw * sizeof(uint16_t);
-    if (!set_lds((const void *)k_env_obs, lds)) return SL_ETOOBIG;
-    hipLaunchKernelGGL(k_env_obs, dim3((unsigned)st->B), dim3(NT), lds, s, *st, a, out);
-    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+    const int rc = obs_args(vh, vw, remove_white_goals, obs_mode, channels, nch, &a);
+    if (rc) return rc;
+    return launch_obs(*st, a, out, (hipStream_t)stream);
 }

@@ -241,13 +241,20 @@ struct FastExtra {
     int32_t fuse_reset;     // auto-reset: the step kernel lists finished envs and a
                             // follow-up kernel resets exactly those
     int64_t *scratch;       // sl_env_cfg.scratch (reset list + counters)
+    uint16_t *obs_out;      // 64x64 kernel: packed views written from the on-chip
+    int32_t obs_vh, obs_vw, obs_rw;   // board (NULL: none); view shape, remove_white
 };
+// packed views of the envs queued for reset in the scratch list of step `step`
+// (after their reset), one wave each (sl_env.hip)
+int launch_obs_packed_list(const sl_env_state &st, int vh, int vw, int remove_white,
+                           uint16_t *out, const int64_t *scratch, uint32_t step, hipStream_t s);
 bool fast_shape(int H, int W);
 int launch_step_fast(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
 // true when the launched fast kernel also performed the auto-resets
 bool launch_fast_fuses_reset(const sl_env_state &st, const FastExtra &fx);
+bool launch_fast_fuses_obs();
 // bit-sliced 128x128 kernel (sl_bits128.hip); needs the goals mirror (st.planes).
 // With fx.fuse_reset it queues the envs that finished and launches
 // k_env_reset_list_wide for them.

@@ -583,6 +583,9 @@ bool launch_fast_fuses_reset(const sl_env_state &st, const FastExtra &fx) {
     return SL_FAST_IMPL == 2 && fx.fuse_reset && fx.pool.K > 0;
 }
 
+// the 64x64 bit-sliced kernel writes packed observations itself (FastExtra.obs_out)
+bool launch_fast_fuses_obs() { return SL_FAST_IMPL == 2; }
+
 int launch_step_fast(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {

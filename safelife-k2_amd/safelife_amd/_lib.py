@@ -60,7 +60,9 @@ class EnvCfg(ctypes.Structure):
                 ("rng_mode", i32), ("seed", u64), ("step", u32), ("env0", u32),
                 ("draws", vp), ("n_draws", i64), ("stream_pos", vp), ("scratch", vp),
                 ("level_mode", i32), ("n_total_envs", i32), ("augment_roll", i32),
-                ("ev_begin", vp), ("ev_end", vp), ("kernel", i32)]
+                ("ev_begin", vp), ("ev_end", vp), ("kernel", i32),
+                ("obs_out", vp), ("obs_mode", i32), ("obs_vh", i32), ("obs_vw", i32),
+                ("obs_remove_white", i32), ("obs_nch", i32), ("obs_channels", i32 * 16)]
 
 
 _lib = None

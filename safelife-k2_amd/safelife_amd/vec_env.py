@@ -239,12 +239,7 @@ class SafeLifeVecEnv:
         vh, vw = self.view_shape
         ch = self._channels if self.obs_mode != _lib.SL_OBS_PACKED else None
         nch = len(self.output_channels) if self.output_channels else 0
-        if out is None:
-            out = self.obs
-        elif (out.shape != self.obs.shape or out.dtype != self.obs.dtype
-              or out.device != self.device or not out.is_contiguous()):
-            raise ValueError("obs out must be a contiguous %s %s tensor on %s"
-                             % (tuple(self.obs.shape), self.obs.dtype, self.device))
+        out = self.obs if out is None else self._obs_target(out)
         _lib.check(L.sl_env_obs(ctypes.byref(self._state), vh, vw, int(self.remove_white_goals),
                                 self.obs_mode, ch, nch, out.data_ptr(),
                                 _lib.stream_ptr(self.device)), "sl_env_obs")
@@ -279,6 +274,12 @@ class SafeLifeVecEnv:
         self._actions_in_flight = a
         L = _lib.lib()
         cfg = self._fill_cfg()
+        # the observation is written by sl_env_step itself (from the on-chip board
+        # where the kernel allows it)
+        obs = None
+        if self.compute_obs or obs_out is not None:
+            obs = self.obs if obs_out is None else self._obs_target(obs_out)
+        self._fill_obs_cfg(cfg, obs)
         _lib.check(L.sl_env_step(ctypes.byref(self._state), ctypes.byref(self._pool_dev["struct"]),
                                  a.data_ptr(), ctypes.byref(cfg),
                                  self._out(reward_out, self.reward).data_ptr(),
@@ -290,8 +291,24 @@ class SafeLifeVecEnv:
                    "sl_env_step")
         self._step_index += 1
         self.global_counter.num_steps += self.B
-        if self.compute_obs or obs_out is not None:
-            self.observe(obs_out)
+
+    def _fill_obs_cfg(self, cfg, out):
+        cfg.obs_out = None if out is None else out.data_ptr()
+        vh, vw = self.view_shape
+        cfg.obs_mode = self.obs_mode
+        cfg.obs_vh, cfg.obs_vw = vh, vw
+        cfg.obs_remove_white = int(self.remove_white_goals)
+        chs = self.output_channels or ()
+        cfg.obs_nch = len(chs)
+        for k, c in enumerate(chs):
+            cfg.obs_channels[k] = c
+
+    def _obs_target(self, out):
+        if (out.shape != self.obs.shape or out.dtype != self.obs.dtype
+                or out.device != self.device or not out.is_contiguous()):
+            raise ValueError("obs out must be a contiguous %s %s tensor on %s"
+                             % (tuple(self.obs.shape), self.obs.dtype, self.device))
+        return out
 
     def _out(self, t, default):
         if t is None:

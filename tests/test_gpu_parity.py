@@ -318,6 +318,44 @@ def test_fast_kernel_vs_generic(torch_dev, spawners):
             _compare_state(fast, gen, t)
 
 
+@pytest.mark.parametrize("view,remove_white,auto_reset,hi_bits", [((33, 33), True, True, False),
+                                                                  ((1, 1), False, True, False),
+                                                                  ((70, 9), True, False, False),
+                                                                  ((7, 64), False, True, False),
+                                                                  ((64, 64), True, True, False),
+                                                                  ((33, 33), True, True, True)])
+def test_fast_kernel_fused_obs(torch_dev, view, remove_white, auto_reset, hi_bits):
+    """The 64x64 kernel writes packed views from the board it holds on chip (views of
+    envs reset after the step are rewritten by a list kernel): every step they equal
+    the stand-alone observation kernel's view of the state left behind (views wider
+    than the board wrap; white goals kept or removed; with and without resets; boards
+    using the otherwise unused cell bits 12-14)."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv
+    path = os.path.join(GOLDEN, "pools", "c3_prune_still_64.npz")
+    pool = _sprinkled_pool(path, np.random.RandomState(4), spawn_frac=0.006)
+    pool.goals[:, 5:9, 5:9] = 0x0E00 | 0x10     # white goal patch in every level
+    if hi_bits:     # unused cell bits 12-14 set on walls: the kernel's bit-sliced add path
+        walls = (pool.board & 0x10) != 0
+        pool.board[walls] |= np.uint16(0x7000)
+    B, T = 130, 50
+    venv = SafeLifeVecEnv(pool, B, "cuda:0", kernel="fast", view_shape=view,
+                          output_channels=None, remove_white_goals=remove_white,
+                          time_limit=17, auto_reset=auto_reset, rng="philox", seed=31,
+                          level_order="random", augment_roll=True, min_performance=0.01)
+    venv.reset()
+    rng = np.random.RandomState(8)
+    resets = 0
+    for t in range(T):
+        a = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+        o, _, _, info = venv.step(a)
+        fused = o.clone()
+        resets += int(info["reset"].sum().item()) if auto_reset else 0
+        ref = venv.observe().clone()
+        assert torch.equal(fused, ref), (t, (fused != ref).nonzero()[:5].tolist())
+    assert resets > 0 or not auto_reset
+
+
 def test_fast_kernel_spawners_vs_oracle(torch_dev):
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv
