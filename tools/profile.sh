@@ -22,3 +22,7 @@ run write --kernel-trace --pmc WRITE_SIZE || exit 1
 run sq1 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES || exit 1
 run sq2 --kernel-trace --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE || exit 1
 python3 $R/tools/pmc_summary.py $OUT --last $STEPS > $OUT/summary.json
+# the per-launch traces are large (gpurun copies back at most 64 MiB): keep the
+# kernel-trace pass's stats and the summary, drop the PMC passes' raw CSVs
+for n in fetch write sq1 sq2; do find $OUT/$n -name "*counter_collection.csv" -delete; find $OUT/$n -name "*kernel_trace.csv" -delete; done
+find $OUT/kt -name "*kernel_trace.csv" -size +8M -exec gzip {} \;
