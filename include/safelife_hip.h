@@ -54,8 +54,9 @@ extern "C" {
 #define SL_RNG_STREAM 0     /* replay a supplied uniform stream (reference order) */
 #define SL_RNG_PHILOX 1     /* counter-based Philox4x32-10 (production) */
 
-#define SL_KERNEL_AUTO 0     /* bit-sliced kernels for 64x64 and 128x128 in
-                                Philox mode, the generic kernel otherwise    */
+#define SL_KERNEL_AUTO 0     /* bit-sliced kernels for 64x64, 128x128 and boards
+                                up to 32x64 in Philox mode, the generic kernel
+                                otherwise                                    */
 #define SL_KERNEL_GENERIC 1  /* LDS-staged per-cell kernel, any shape        */
 #define SL_KERNEL_FAST 2     /* require the fast kernel (error if none)      */
 

@@ -58,6 +58,13 @@ namespace {
 #ifndef SL_BITS_MINW
 #define SL_BITS_MINW 4       // waves per SIMD the register budget is sized for
 #endif
+#ifndef SL_BITS_PERSIST
+#define SL_BITS_PERSIST 0    // persistent waves: the next env's board, record and goal
+                             // colour planes are loaded while this env finishes
+#endif
+#ifndef SL_BITS_WAVES_PER_CU
+#define SL_BITS_WAVES_PER_CU 16   // persistent grid: waves per CU
+#endif
 #ifndef SL_BITS_MINW_OBS
 #define SL_BITS_MINW_OBS 3   // the same for the instantiation that writes observations
 #endif
@@ -377,13 +384,37 @@ __device__ __forceinline__ void write_obs(lds_u32 *buf, const FastExtra &fx, con
     }
 }
 
-template <bool OBS>
+// What an env's step needs first, issued ahead: the per-env record (lane k = field k)
+// and the goals' three colour planes from the mirror (speculative: used when the
+// mirror is valid).  The board itself is DMA'd into the wave's LDS buffer.
+struct Pre {
+    u32 V;
+    u32 g[3][2];
+};
+
+__device__ __forceinline__ void issue_pre(const sl_env_state &st, const int32_t *actions,
+                                          int64_t b, int lane, Pre &p) {
+    p.V = load_record(st, actions, b, lane);
+    if (SL_BITS_MIRROR && st.planes) {
+        const u32 *mg = st.planes + b * 4096 + 2048 + lane;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            p.g[k][0] = mg[(9 + k) * 64];
+            p.g[k][1] = mg[(25 + k) * 64];
+        }
+    }
+}
+
+// One env-step of env b.  `pre` holds b's record and goal colour planes and b's board
+// is in flight into `buf` (issued by the caller).  With PF, the same is issued for
+// env bn (< 0: none) as soon as this env no longer needs the buffer / registers.
+template <bool OBS, bool PF>
 __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs &a,
                                          const FastExtra &fx, int64_t b, int lane, lds_u32 *buf,
                                          const int32_t *__restrict__ actions, int ctp, int ctc,
                                          double *reward_out, uint8_t *done_out,
                                          uint8_t *flags_out, int32_t *ep_len_out,
-                                         int32_t *ep_rew_out) {
+                                         int32_t *ep_rew_out, Pre &pre, int64_t bn) {
     const int64_t off = b * (int64_t)(N * N);
     const int lane_off = (lane & 1) * 1024 + (lane >> 1);     // dwords: row 32h, column pair j
     u32 *gb = reinterpret_cast<u32 *>(st.board + off) + lane_off;
@@ -393,19 +424,16 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     // (the goals rarely change, so it saves their transpose at almost no write cost;
     // a board mirror would be rewritten every step and does not pay)
     u32 *mg = (SL_BITS_MIRROR && st.planes) ? st.planes + b * 4096 + 2048 + lane : nullptr;
-    const u32 V = load_record(st, actions, b, lane);           // issued first
-    dma_board(st.board + off, buf, lane);                       // board cells -> LDS
+    const u32 V = pre.V;
     // goals: a goals board without spawners that came through a step unchanged is at
     // a fixed point of the (then deterministic) rule and never changes again
     // (planes_ok bit 2); such envs read only the three colour planes of the mirror,
     // which are speculatively in flight before the record says which case holds
     u32 gcol[3][2];                    // goal colour planes, kept for the scores
-    if (mg) {
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            gcol[k][0] = mg[(9 + k) * 64];
-            gcol[k][1] = mg[(25 + k) * 64];
-        }
+    for (int k = 0; k < 3; k++) {
+        gcol[k][0] = pre.g[k][0];
+        gcol[k][1] = pre.g[k][1];
     }
     const int pok = (mg && st.planes_ok) ? rec(V, R_POK) & 6 : 0;
 
@@ -533,6 +561,10 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     // reduced before the board store so the scoring is not sunk past it
     const int s1 = wave_total((pts + 192) | ((scr + 64) << 16));
     const int s2 = wave_total(pos | (side << 16));
+    if (PF && !OBS && bn >= 0) {        // the buffer has been read out: next env's board
+        wait_lgkm();
+        dma_board(st.board + bn * (int64_t)(N * N), buf, lane);
+    }
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- write back the changed rows of the board, exits already in the colour the
@@ -592,6 +624,13 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         write_obs(buf, fx, fl, b, lane);
         __builtin_amdgcn_sched_barrier(0);
     }
+    if (PF && bn >= 0) {
+        if (OBS) {
+            wait_lgkm();
+            dma_board(st.board + bn * (int64_t)(N * N), buf, lane);
+        }
+        issue_pre(st, actions, bn, lane, pre);
+    }
     int reset = 0;
     if (!(SL_BITS_ABL & 16) && (SL_BITS_UEPI || lane == 0))
         reset = epilogue_core(st, a, b, fl, act_reward, points, score, possible, side_total,
@@ -606,20 +645,51 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
 }
 
 // OBS: also write the packed observation (fx.obs_out)
+// all kernel arguments in one struct at kernarg offset 0 (see the persistent loop)
+struct StepKArgs {
+    sl_env_state st;
+    StepArgs a;
+    FastExtra fx;
+    const int32_t *actions;
+    int ctp, ctc;
+    double *reward_out;
+    uint8_t *done_out, *flags_out;
+    int32_t *ep_len_out, *ep_rew_out;
+};
+
 template <bool OBS>
 __global__ void __launch_bounds__(64 * SL_BITS_WPB, OBS ? SL_BITS_MINW_OBS : SL_BITS_MINW)
-k_env_step_bits64(sl_env_state st, StepArgs a, FastExtra fx, const int32_t *__restrict__ actions, int ctp,
-                  int ctc, double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
-                  uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
-                  int32_t *__restrict__ ep_rew_out) {
+k_env_step_bits64(StepKArgs ka) {
     const int64_t b = (int64_t)blockIdx.x * SL_BITS_WPB +
                       __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     __shared__ __attribute__((aligned(16))) u32 stage[SL_BITS_WPB][N * N / 2];
-    if (b >= st.B) return;                 // whole waves only
+    if (b >= ka.st.B) return;              // whole waves only
     lds_u32 *buf = (lds_u32 *)&stage[threadIdx.x >> 6][0];
-    step_env<OBS>(st, a, fx, b, lane, buf, actions, ctp, ctc, reward_out, done_out, flags_out,
-                  ep_len_out, ep_rew_out);
+    Pre pre;
+    issue_pre(ka.st, ka.actions, b, lane, pre);
+    dma_board(ka.st.board + b * (int64_t)(N * N), buf, lane);
+    if (SL_BITS_PERSIST) {
+        // persistent waves, static stride over the envs; every wave leaves the loop
+        // after at most ceil(B / waves) iterations.  The arguments are re-read from
+        // the kernarg segment in every iteration through a pointer the compiler cannot
+        // see as loop-invariant: hoisted, the ~60 argument dwords would not fit in
+        // the SGPR file next to the step's own scalars and would spill.
+        const int G = (int)gridDim.x * SL_BITS_WPB, nb = (int)ka.st.B;     // B < 2^31
+        for (int e = (int)b; e < nb; e += G) {
+            auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(kp));
+            const StepKArgs &k = *(const StepKArgs *)kp;
+            const int en = e + G < nb ? e + G : -1;
+            step_env<OBS, true>(k.st, k.a, k.fx, e, lane, buf, k.actions, k.ctp, k.ctc,
+                                k.reward_out, k.done_out, k.flags_out, k.ep_len_out, k.ep_rew_out,
+                                pre, en);
+        }
+    } else {
+        step_env<OBS, false>(ka.st, ka.a, ka.fx, b, lane, buf, ka.actions, ka.ctp, ka.ctc,
+                             ka.reward_out, ka.done_out, ka.flags_out, ka.ep_len_out,
+                             ka.ep_rew_out, pre, -1);
+    }
 }
 
 // Resets the envs the step kernel queued (one wave per env, grid-stride over the
@@ -643,14 +713,26 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (st.H != N || st.W != N) return SL_ETOOBIG;
-    const unsigned grid = (unsigned)((st.B + SL_BITS_WPB - 1) / SL_BITS_WPB);
+    unsigned grid = (unsigned)((st.B + SL_BITS_WPB - 1) / SL_BITS_WPB);
+    if (SL_BITS_PERSIST) {
+        static int n_cu = 0;           // per process; one device type (gfx950)
+        if (n_cu == 0) {
+            int dev = 0, v = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                v <= 0)
+                v = 256;
+            n_cu = v;
+        }
+        const unsigned cap = (unsigned)(n_cu * SL_BITS_WAVES_PER_CU / SL_BITS_WPB);
+        if (grid > cap) grid = cap;
+    }
+    const StepKArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
     if (fx.obs_out) {
         if (fx.obs_vh < 1 || fx.obs_vw < 1 || fx.obs_vh * fx.obs_vw > 4096) return SL_EINVAL;
-        hipLaunchKernelGGL(k_env_step_bits64<true>, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, st,
-                           a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+        hipLaunchKernelGGL(k_env_step_bits64<true>, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, ka);
     } else {
-        hipLaunchKernelGGL(k_env_step_bits64<false>, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, st,
-                           a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+        hipLaunchKernelGGL(k_env_step_bits64<false>, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, ka);
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.fuse_reset && fx.pool.K > 0) {

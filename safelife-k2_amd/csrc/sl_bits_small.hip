@@ -1,0 +1,306 @@
+// sl_bits_small.hip -- the bit-sliced fused env-step kernel for small boards
+// (H <= 32, W <= 64: BASELINE config C2's 25x25 proc-gen levels, the 26x26 v1.0
+// benchmark levels).
+//
+// Same semantics as k_env_action + k_env_step_generic (sl_env.hip); the layout is the
+// 64x64 kernel's (sl_bits.hip) folded to one row band:
+//
+//  * one wave64 per env; lane j < nl = ceil(W / 2) owns the column pair (2j, 2j+1)
+//    over ALL rows: bit y of plane k, word w = bit k of cell(y, 2j + w), so a whole
+//    board is 16 planes x 2 words per lane and the rule (sl_bits.h rule_planes,
+//    SURVEY.md Appendix A / advance_board.c:34-120) runs on 2 x H cells per op;
+//  * vertical neighbours are rotations within the low H bits (the torus wrap at H);
+//  * horizontal neighbours come from the neighbouring column pairs through
+//    ds_bpermute, which wraps at W for any W (the whole-wave DPP rotations of the
+//    64x64 kernel wrap at 64 lanes only).  For odd W the last lane's second word is
+//    a copy of column 0 -- exactly the right neighbour its first word needs -- and
+//    everything it computes for that word is discarded;
+//  * the action (execute_action / move_agent, safelife_game.py:308-393) runs on lane
+//    0 against the board staged in LDS; its edits are muxed into the planes;
+//  * points, performance score, possible score and side effects
+//    (safelife_game.py:590-631, env_wrappers.py:319-342) are recomputed in full from
+//    the planes; only changed rows are stored; the epilogue is the shared one.
+// Resets after the step are done by k_env_reset_scan (sl_env.hip).  Philox mode only.
+#include "sl_bits.h"
+
+using namespace sl;
+using namespace sl::fast;
+using namespace sl::bits;
+
+namespace {
+
+constexpr int kMaxH = 32, kMaxW = 64;
+
+struct GeoSmall {
+    int lane, H, W, nl;
+    u32 mh;                  // the low H bits
+    int src_l, src_r;        // lanes holding columns 2j - 1 and 2j + 2
+    bool odd_last;           // this lane's word 1 is the column-0 copy (odd W)
+    template <class F>
+    __device__ __forceinline__ V3 vert(const u32 *P, int w, F f) const {
+        const u32 x = f(P, w);
+        return V3{((x << 1) | (x >> (H - 1))) & mh, ((x >> 1) | ((x & 1u) << (H - 1))) & mh};
+    }
+    __device__ __forceinline__ H3 horiz(u32 w0, u32 w1) const {
+        const u32 right_col = odd_last ? w0 : w1;          // this lane's last real column
+        return H3{(u32)__builtin_amdgcn_ds_bpermute(4 * src_l, (int)right_col),
+                  (u32)__builtin_amdgcn_ds_bpermute(4 * src_r, (int)w0)};
+    }
+    __device__ __forceinline__ bool halo_spawn() const { return false; }
+    __device__ __forceinline__ u32 cell(int y, int w) const { return (u32)(y * W + 2 * lane + w); }
+    __device__ __forceinline__ void draws(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
+                                          u32 tensor) const {
+        lane_draws(*this, elig, sp, sc, tensor);
+    }
+};
+
+typedef __attribute__((address_space(3))) u32 lds_u32;
+typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
+
+// unedited cells for the action, from the staged board: row y is 32 dwords, cell
+// (y, x) the u16 at y * 64 + x
+struct SmallCells {
+    const lds_u32 *buf;
+    int W;
+    __device__ __forceinline__ uint32_t operator()(int i) const {
+        const int y = i / W, x = i - y * W;
+        return reinterpret_cast<lds_cu16 *>(buf)[y * 64 + x];
+    }
+};
+
+// Board, goals and start board are staged in LDS as rows of 64 u16 (cell (y, x) at
+// y * 64 + x), each tensor read by the whole wave with coalesced u16 loads (cells
+// lane + 64 k), eight per lane and tensor in flight at once.  For odd W column 0 is
+// also written at x = W, so the last lane's second word reads as its copy.
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+constexpr int kGroup = 8;
+
+__device__ __forceinline__ void stage_tensors(const uint16_t *const src[3], lds_u16 *const dst[3],
+                                              int HW, int W, int lane) {
+    const int dy = 64 / W, dx = 64 - dy * W;
+    int y = lane / W, x = lane - (lane / W) * W;
+    for (int i0 = lane; i0 < HW; i0 += 64 * kGroup) {
+        uint32_t v[3][kGroup];
+        int pos[kGroup];
+#pragma unroll
+        for (int g = 0; g < kGroup; g++) {
+            const int i = i0 + 64 * g;
+            pos[g] = -1;
+            if (i < HW) {
+#pragma unroll
+                for (int t = 0; t < 3; t++) v[t][g] = src[t][i];
+                pos[g] = y * 64 + x + ((x == 0 && (W & 1)) ? 0x10000 : 0);
+            }
+            y += dy;
+            x += dx;
+            if (x >= W) {
+                x -= W;
+                y++;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < kGroup; g++)
+            if (pos[g] >= 0) {
+                const int p = pos[g] & 0xFFFF;
+#pragma unroll
+                for (int t = 0; t < 3; t++) {
+                    dst[t][p] = (uint16_t)v[t][g];
+                    if (pos[g] >> 16) dst[t][p + W] = (uint16_t)v[t][g];    // column-0 copy
+                }
+            }
+    }
+}
+
+// the lane's dwords D[y] = cell(y, 2j) | cell(y, 2j + 1) << 16 (0 outside the board)
+__device__ __forceinline__ void lds_rows(const lds_u16 *t, int H, bool active, int lane,
+                                         u32 D[32]) {
+    const lds_u32 *p = reinterpret_cast<const lds_u32 *>(t) + lane;
+#pragma unroll
+    for (int y = 0; y < kMaxH; y++) D[y] = (active && y < H) ? p[y * 32] : 0u;
+}
+
+#ifndef SL_SMALL_MINW
+#define SL_SMALL_MINW 3      // waves per SIMD (the 12 KiB LDS stage allows 3.25)
+#endif
+
+__global__ void __launch_bounds__(64, SL_SMALL_MINW)
+k_env_step_small(sl_env_state st, StepArgs a, const int32_t *__restrict__ actions, int ctp,
+                 int ctc, double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
+                 uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
+                 int32_t *__restrict__ ep_rew_out) {
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int H = st.H, W = st.W, nl = (W + 1) >> 1;
+    __shared__ __attribute__((aligned(16))) u32 stage[3][kMaxH * 32];   // board, goals, start
+    lds_u32 *buf = (lds_u32 *)stage[0];
+    const bool active = lane < nl;
+    const int c0 = 2 * lane, c1 = 2 * lane + 1;             // stores: c1 < W unless odd_last
+    GeoSmall geo;
+    geo.lane = lane;
+    geo.H = H;
+    geo.W = W;
+    geo.nl = nl;
+    geo.mh = H == 32 ? ~0u : ((1u << H) - 1u);
+    geo.src_l = active ? (lane == 0 ? nl - 1 : lane - 1) : lane;
+    geo.src_r = active ? (lane + 1 == nl ? 0 : lane + 1) : lane;
+    geo.odd_last = (W & 1) && lane == nl - 1;
+    // valid cells per word: rows < H of real columns
+    const u32 wm0 = active ? geo.mh : 0u, wm1 = (active && !geo.odd_last) ? geo.mh : 0u;
+
+    const int64_t off = b * (int64_t)H * W;
+    const u32 V = load_record(st, actions, b, lane);
+    {
+        const uint16_t *src[3] = {st.board + off, st.goals + off, st.start_board + off};
+        lds_u16 *dst[3] = {(lds_u16 *)stage[0], (lds_u16 *)stage[1], (lds_u16 *)stage[2]};
+        // rows of odd boards end in the column-0 copy; the rest of a row stays unread
+        stage_tensors(src, dst, H * W, W, lane);
+    }
+    wait_lgkm();
+    u32 PB[32], PG[32];
+    lds_rows((const lds_u16 *)stage[1], H, active, lane, PG);
+
+    SpawnCtx sc;
+    sc.gid = a.env0 + (uint32_t)b;
+    sc.step = a.step;
+    sc.seed = a.seed;
+    sc.thr = (double)__int_as_float(rec(V, R_SPAWN));
+
+    // ---- goals: rule, then store the changed rows
+    transpose32(PG);
+    u32 cg[2];
+    rule_planes(PG, cg, geo, sc, 1u);
+    cg[0] &= wm0;
+    cg[1] &= wm1;
+    const u32 rg = wave_or(cg[0] | cg[1]);
+    u32 gcol[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        gcol[k][0] = PL(PG, 9 + k, 0) & wm0;
+        gcol[k][1] = PL(PG, 9 + k, 1) & wm1;
+    }
+    if (rg) {
+        transpose32(PG);
+        uint16_t *gg = st.goals + off;
+#pragma unroll
+        for (int y = 0; y < kMaxH; y++)
+            if (((rg >> y) & 1u) && active) {
+                gg[y * W + c0] = (uint16_t)PG[y];
+                if (!geo.odd_last) gg[y * W + c1] = (uint16_t)(PG[y] >> 16);
+            }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- board: the action reads the staged cells, then the rows become planes
+    OverlayT<SmallCells> ov;
+    ov.src.buf = buf;
+    ov.src.W = W;
+    ov.n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        ov.idx[k] = 0;
+        ov.val[k] = 0;
+    }
+    RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
+               rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
+    int act_reward = 0;
+    if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), H, W, ctp, ctc, ov);
+    act_reward = __builtin_amdgcn_readfirstlane(act_reward);
+    const int ne = __builtin_amdgcn_readfirstlane(ov.n);
+    int eidx[4];
+    u32 eval[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        eidx[k] = __builtin_amdgcn_readfirstlane(ov.idx[k]);
+        eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
+    }
+    RecFields fl{V, __builtin_amdgcn_readfirstlane(env.go), __builtin_amdgcn_readfirstlane(env.ax),
+                 __builtin_amdgcn_readfirstlane(env.ay), 0.0};
+    if (a.bonus_period > 0)
+        fl.bval = a.bonus_table[bonus_dist(fl.ax, fl.ay, fl.prior_x(fl.prior_head()),
+                                           fl.prior_y(fl.prior_head()), fl.prior_len(),
+                                           a.bonus_period, a.bonus_len)];
+    lds_rows((const lds_u16 *)stage[0], H, active, lane, PB);
+    transpose32(PB);
+    u32 erow = 0;                              // rows holding an edit
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (k < ne) {
+            const int y = eidx[k] / W, x = eidx[k] - (eidx[k] / W) * W;
+            const u32 bit = 1u << y;
+            // the cell's word, and for x = 0 with odd W also the last lane's copy
+            const u32 m0 = (lane == (x >> 1) && !(x & 1)) ? bit : 0u;
+            const u32 m1 = ((lane == (x >> 1) && (x & 1)) || (x == 0 && geo.odd_last)) ? bit : 0u;
+            erow |= bit;
+#pragma unroll
+            for (int p = 0; p < 16; p++) {
+                const u32 v = ((eval[k] >> p) & 1u) ? ~0u : 0u;
+                PL(PB, p, 0) = mux(m0, v, PL(PB, p, 0));
+                PL(PB, p, 1) = mux(m1, v, PL(PB, p, 1));
+            }
+        }
+    }
+    u32 cb[2];
+    rule_planes(PB, cb, geo, sc, 0u);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- scores over the real cells of the new board and goals
+    u32 PS[32];
+    lds_rows((const lds_u16 *)stage[2], H, active, lane, PS);
+    transpose32(PS);
+#pragma unroll
+    for (int p = 0; p < 16; p++) {
+        PL(PB, p, 0) &= wm0;
+        PL(PB, p, 1) &= wm1;
+        PL(PS, p, 0) &= wm0;
+        PL(PS, p, 1) &= wm1;
+    }
+    int pts, scr, pos, side;
+    score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
+    const int s1 = wave_total((pts + 192) | ((scr + 64) << 16));
+    const int s2 = wave_total(pos | (side << 16));
+    const int points = (s1 & 0xFFFF) - 192 * 64;
+    const int score = ((s1 >> 16) & 0xFFFF) - 64 * 64;
+    const int possible = s2 & 0xFFFF;
+    const int side_total = (s2 >> 16) & 0xFFFF;
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- changed rows, exits in the colour the epilogue gives them
+    const u32 rb = wave_or((cb[0] & wm0) | (cb[1] & wm1)) | erow;
+    if (rb) {
+        const bool can = can_exit_now(fl.min_performance(), score, fl.baseline(), possible);
+#pragma unroll
+        for (int w = 0; w < 2; w++)
+            PL(PB, 9, w) = can ? (PL(PB, 9, w) | PL(PB, 8, w)) : (PL(PB, 9, w) & ~PL(PB, 8, w));
+        transpose32(PB);
+        uint16_t *gb = st.board + off;
+#pragma unroll
+        for (int y = 0; y < kMaxH; y++)
+            if (((rb >> y) & 1u) && active) {
+                gb[y * W + c0] = (uint16_t)PB[y];
+                if (!geo.odd_last) gb[y * W + c1] = (uint16_t)(PB[y] >> 16);
+            }
+    }
+    if (lane == 0)
+        epilogue_core(st, a, b, fl, act_reward, points, score, possible, side_total, reward_out,
+                      done_out, flags_out, ep_len_out, ep_rew_out);
+}
+
+}  // namespace
+
+namespace sl {
+
+bool small_shape(const sl_env_state &st) {
+    return st.H >= 2 && st.H <= kMaxH && st.W >= 2 && st.W <= kMaxW;
+}
+
+int launch_step_small(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
+                      int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
+                      int32_t *ep_rew, hipStream_t s) {
+    if (!small_shape(st)) return SL_ETOOBIG;
+    if (st.B > 0x7FFFFFFF) return SL_EINVAL;
+    hipLaunchKernelGGL(k_env_step_small, dim3((unsigned)st.B), dim3(64), 0, s, st, a, actions, ctp,
+                       ctc, reward, done, flags, ep_len, ep_rew);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
+}  // namespace sl

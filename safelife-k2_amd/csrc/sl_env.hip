@@ -990,7 +990,8 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     const bool philox_fast = cfg->rng_mode == SL_RNG_PHILOX && cfg->kernel != SL_KERNEL_GENERIC;
     const bool fast = philox_fast && fast_shape(st->H, st->W);
     const bool fast128 = philox_fast && bits128_shape(*st);
-    if (cfg->kernel == SL_KERNEL_FAST && !fast && !fast128) return SL_ETOOBIG;
+    const bool small = philox_fast && !fast && small_shape(*st);
+    if (cfg->kernel == SL_KERNEL_FAST && !fast && !fast128 && !small) return SL_ETOOBIG;
     bool reset_done = false;
     FastExtra fx;
     fx.fuse_reset = cfg->auto_reset ? 1 : 0;
@@ -1018,6 +1019,11 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
                                      ep_reward, s);
         if (rc) return rc;
         reset_done = fx.fuse_reset && fx.pool.K > 0;
+    } else if (small) {
+        if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
+        int rc = launch_step_small(*st, a, actions, cfg->can_toggle_powers, cfg->can_toggle_colors,
+                                   reward, done, info_flags, ep_len, ep_reward, s);
+        if (rc) return rc;
     } else if (fast) {
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
         int rc = launch_step_fast(*st, a, fx, actions, cfg->can_toggle_powers,

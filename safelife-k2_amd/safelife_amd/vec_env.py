@@ -165,6 +165,9 @@ class SafeLifeVecEnv:
                              % (pool.H, pool.W, self.H, self.W))
         self.pool = pool
         self._pool_dev = pool.to_device(self.device)
+        # running episodes' start boards are no longer levels of the pool: the
+        # kernels read them from HBM until those envs are reset from the new pool
+        self.st_t["start_roll"].fill_(-1)
 
     def set_spawn_stream(self, stream, pos=0):
         """Uniform doubles consumed in reference order (rng='stream')."""

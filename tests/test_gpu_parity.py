@@ -424,8 +424,9 @@ def test_full_batch_sampled_vs_oracle(torch_dev):
 
 def test_fast_kernel_state_overwrite(torch_dev):
     """set_state mid-run (board/goals/start written by the caller) invalidates the fast
-    kernel's bit-plane mirrors and pool start-board source: the run continues bit-exact
-    with the generic kernel given the same overwrite."""
+    kernel's bit-plane mirrors and pool start-board source, and so does set_pool (a new
+    level pool while episodes run): the run continues bit-exact with the generic kernel
+    given the same overwrite."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
     path = os.path.join(GOLDEN, "pools", "c3_prune_still_64.npz")
@@ -450,10 +451,70 @@ def test_fast_kernel_state_overwrite(torch_dev):
                   if k != "start_roll"}
             fast.set_state(bd, gl, sb, **sc)
             gen.set_state(bd, gl, sb, **sc)
+        if t == 45:
+            # a new level pool mid-episode: running episodes keep their start boards
+            newpool = LevelPool.load(path).subset(np.arange(31, -1, -1) % 32)
+            fast.set_pool(newpool)
+            gen.set_pool(newpool)
         _, r1, d1, _ = fast.step(a)
         _, r2, d2, _ = gen.step(a)
         assert torch.equal(r1, r2), t
         assert torch.equal(d1, d2), t
+        _compare_state(fast, gen, t)
+
+
+# ------------------------------------------- small-board bit-sliced kernel (C2)
+def _synthetic_pool(rng, K, H, W):
+    """K random levels of any shape: life of random colours, walls, crates, spawners,
+    an agent and an exit, colour goals (some live)."""
+    from safelife_amd import LevelPool
+    board = _random_boards(rng, K, H, W)
+    goals = np.where(rng.rand(K, H, W) < 0.3, rng.randint(1, 8, size=(K, H, W)) << 9, 0)
+    goals = (goals | np.where(rng.rand(K, H, W) < 0.05, 9, 0)).astype(np.uint16)
+    al = np.zeros((K, 2), np.int64)
+    for k in range(K):
+        ax, ay = rng.randint(0, W), rng.randint(0, H)
+        ex, ey = (ax + W // 2) % W, (ay + H // 2) % H
+        board[k, ay, ax] = 122
+        if (ex, ey) != (ax, ay):
+            board[k, ey, ex] = 272
+        al[k] = (ax, ay)
+    return LevelPool(board, goals, al, rng.randint(0, 4, size=K), np.full(K, 0.3),
+                     np.full(K, 0.01))
+
+
+@pytest.mark.parametrize("shape", [(25, 25), (26, 26), (2, 2), (3, 5), (32, 63), (17, 64),
+                                   (31, 2)])
+def test_small_kernel_vs_generic(torch_dev, shape):
+    """Boards up to 32x64 take the bit-sliced small kernel (column pairs over all rows,
+    ds_bpermute wrap at W, odd W via a column-0 copy): bit-exact with the generic
+    kernel through actions, spawns, exits and resets."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    H, W = shape
+    rng = np.random.RandomState(H * 100 + W)
+    if shape == (25, 25):
+        pool = _sprinkled_pool(os.path.join(GOLDEN, "pools", "c2_append_still_25.npz"), rng,
+                               spawn_frac=0.01)
+    else:
+        pool = _synthetic_pool(rng, 8, H, W)
+    B, T = 96, 70
+    kw = dict(time_limit=23, view_shape=(9, 9), output_channels=None, penalty_coef=0.7,
+              min_performance=0.01, rng="philox", seed=5, level_order="random",
+              augment_roll=True)
+    fast = SafeLifeVecEnv(pool, B, "cuda:0", kernel="fast", **kw)
+    gen = SafeLifeVecEnv(pool, B, "cuda:0", kernel="generic", **kw)
+    o1, o2 = fast.reset(), gen.reset()
+    assert torch.equal(o1, o2)
+    for t in range(T):
+        a = torch.from_numpy(rng.choice(9, size=B, p=[.05] + [.1] * 4 + [.1375] * 4)
+                             .astype(np.int32)).to(dev)
+        o1, r1, d1, _ = fast.step(a)
+        o2, r2, d2, _ = gen.step(a)
+        assert torch.equal(r1, r2), (t, (r1 - r2).abs().max().item())
+        assert torch.equal(d1, d2), t
+        assert torch.equal(fast.flags, gen.flags), t
+        assert torch.equal(o1, o2), t
         _compare_state(fast, gen, t)
 
 

@@ -14,7 +14,7 @@ for spec in "$@"; do
   mkdir -p $tmp
   cp $C/*.hip $C/*.h $tmp/
   cp $src $tmp/sl_bits.hip
-  /opt/rocm/bin/hipcc $FLAGS -DSL_FAST_IMPL=2 $defs $tmp/sl_board.hip $tmp/sl_env.hip $tmp/sl_fast.hip $tmp/sl_bits.hip -o $OUT/$name.so &
+  /opt/rocm/bin/hipcc $FLAGS -DSL_FAST_IMPL=2 $defs $tmp/sl_board.hip $tmp/sl_env.hip $tmp/sl_fast.hip $tmp/sl_bits.hip $tmp/sl_bits128.hip $tmp/sl_bits_small.hip $tmp/sl_rollout.hip -o $OUT/$name.so &
 done
 wait
 ls -la $OUT
