@@ -296,6 +296,28 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
     }
 }
 
+// all kernel arguments of k_env_step_bits64 in one struct at kernarg offset 0, so a
+// phase can re-read one late through kernarg() (see the persistent loop, write_obs)
+struct StepKArgs {
+    sl_env_state st;
+    StepArgs a;
+    FastExtra fx;
+    const int32_t *actions;
+    int ctp, ctc;
+    double *reward_out;
+    uint8_t *done_out, *flags_out;
+    int32_t *ep_len_out, *ep_rew_out;
+};
+
+// the kernel's arguments through a pointer the compiler cannot see as invariant: a
+// field read through it is loaded where it is used, not hoisted into the SGPRs that
+// the whole kernel then has to keep
+__device__ __forceinline__ const StepKArgs &kernarg() {
+    auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return *(const StepKArgs *)kp;
+}
+
 // ---------------------------------------------------------------- fused observation
 // SafeLifeEnv.get_obs + recenter_view (safelife_env.py:125-155, helper_utils.py:41-74)
 // of the board the kernel holds on chip, packed (output_channels=None): the same
@@ -329,8 +351,9 @@ __device__ __forceinline__ void write_obs(lds_u32 *buf, const FastExtra &fx, con
                                           int64_t b, int lane) {
     typedef __attribute__((address_space(3))) uint16_t lds_u16;
     lds_u16 *cells = reinterpret_cast<lds_u16 *>(buf);
-    int vh = fx.obs_vh, vw = fx.obs_vw;
-    asm volatile("" : "+s"(vh), "+s"(vw));   // keeps the view arithmetic from being hoisted
+    (void)fx;
+    const FastExtra &lfx = kernarg().fx;     // read late: no SGPRs held through the step
+    const int vh = lfx.obs_vh, vw = lfx.obs_vw;
     const int nv = vh * vw;
     const int ty = fl.ay - vh / 2, tx = fl.ax - vw / 2;
     // exits onto their clipped view positions: lane k < ne handles exit k (values read
@@ -354,7 +377,7 @@ __device__ __forceinline__ void write_obs(lds_u32 *buf, const FastExtra &fx, con
     if (small)
         for (int k = 0; k < ne; k++)            // one store instruction per exit, in order
             if (lane == k) cells[tgt & 4095] = (uint16_t)val;
-    uint16_t *o = fx.obs_out + b * (int64_t)nv;
+    uint16_t *o = lfx.obs_out + b * (int64_t)nv;
     const int dr = 64 / vw, dc = 64 - dr * vw;
     int r = lane / vw, c = lane - r * vw;
     if (small) {
@@ -582,13 +605,15 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
             PL(PB, 9, w) = can ? (PL(PB, 9, w) | PL(PB, 8, w)) : (PL(PB, 9, w) & ~PL(PB, 8, w));
         const bool hi = OBS && __ballot((PL(PB, 12, 0) | PL(PB, 13, 0) | PL(PB, 14, 0) |
                                          PL(PB, 12, 1) | PL(PB, 13, 1) | PL(PB, 14, 1)) != 0u) != 0ull;
+        const int obs_rw = OBS ? kernarg().fx.obs_rw : 0;
+        const u32(&gv)[3][2] = gcol;
         if (OBS && !hi) {
             // planes 12-14 := goal colours; the store masks them out again
 #pragma unroll
             for (int w = 0; w < 2; w++) {
-                const u32 white = fx.obs_rw ? (gcol[0][w] & gcol[1][w] & gcol[2][w]) : 0u;
+                const u32 white = obs_rw ? (gv[0][w] & gv[1][w] & gv[2][w]) : 0u;
 #pragma unroll
-                for (int k = 0; k < 3; k++) PL(PB, 12 + k, w) = gcol[k][w] & ~white;
+                for (int k = 0; k < 3; k++) PL(PB, 12 + k, w) = gv[k][w] & ~white;
             }
             transpose32(PB);
             if (rb) {
@@ -604,11 +629,11 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
                 transpose32(PB);
 #pragma unroll
                 for (int w = 0; w < 2; w++) {
-                    const u32 white = fx.obs_rw ? (gcol[0][w] & gcol[1][w] & gcol[2][w]) : 0u;
+                    const u32 white = obs_rw ? (gv[0][w] & gv[1][w] & gv[2][w]) : 0u;
                     u32 cy = 0u;
 #pragma unroll
                     for (int k = 0; k < 3; k++) {
-                        const u32 g = gcol[k][w] & ~white, p = PL(PB, 12 + k, w);
+                        const u32 g = gv[k][w] & ~white, p = PL(PB, 12 + k, w);
                         PL(PB, 12 + k, w) = p ^ g ^ cy;
                         cy = maj(p, g, cy);
                     }
@@ -645,18 +670,6 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
 }
 
 // OBS: also write the packed observation (fx.obs_out)
-// all kernel arguments in one struct at kernarg offset 0 (see the persistent loop)
-struct StepKArgs {
-    sl_env_state st;
-    StepArgs a;
-    FastExtra fx;
-    const int32_t *actions;
-    int ctp, ctc;
-    double *reward_out;
-    uint8_t *done_out, *flags_out;
-    int32_t *ep_len_out, *ep_rew_out;
-};
-
 template <bool OBS>
 __global__ void __launch_bounds__(64 * SL_BITS_WPB, OBS ? SL_BITS_MINW_OBS : SL_BITS_MINW)
 k_env_step_bits64(StepKArgs ka) {

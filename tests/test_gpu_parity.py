@@ -385,8 +385,9 @@ def test_fast_kernel_spawners_vs_oracle(torch_dev):
 
 def test_full_batch_sampled_vs_oracle(torch_dev):
     """The headline configuration at full size (B = 65 536 envs of 64x64, fast kernel,
-    PPO chain, Philox): every step, a sample of envs spread over the batch matches the
-    oracle run of the same global env ids bit for bit (board, goals, reward, done), and
+    PPO chain, Philox, 33x33 packed views written by the step kernel): every step, a
+    sample of envs spread over the batch matches the oracle run of the same global env
+    ids bit for bit (board, goals, observation, reward, done), and
     the batch-wide episode counters agree with the reset flags."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
@@ -396,7 +397,7 @@ def test_full_batch_sampled_vs_oracle(torch_dev):
     kw = dict(time_limit=15, view_shape=(33, 33), output_channels=None, penalty_coef=1.0,
               min_performance=0.01)
     venv = SafeLifeVecEnv(LevelPool.load(path), B, "cuda:0", rng="philox", seed=2024,
-                          compute_obs=False, kernel="fast", **kw)
+                          compute_obs=True, kernel="fast", **kw)    # views fused in the kernel
     sample = [0, 1, 63, 4097, 32767, 40000, 65534, 65535]
     oenvs = {e: oracle.OracleEnv(lambda ep, e=e: levels[(e + ep * B) % len(levels)],
                                  env_id=e, rng="philox", seed=2024, **kw) for e in sample}
@@ -408,12 +409,13 @@ def test_full_batch_sampled_vs_oracle(torch_dev):
     n_done = 0
     for t in range(T):
         acts = rng.randint(0, 9, size=B).astype(np.int32)
-        _, vr, vd, info = venv.step(torch.from_numpy(acts).to(dev))
+        vo, vr, vd, info = venv.step(torch.from_numpy(acts).to(dev))
         n_done += int(info["reset"].sum().item())     # times_up and game_over resets
-        vr, vd = vr.cpu().numpy(), vd.cpu().numpy()
+        vo, vr, vd = vo.cpu().numpy(), vr.cpu().numpy(), vd.cpu().numpy()
         for e in sample:
-            _, r, dn, _ = oenvs[e].step(int(acts[e]))
+            o, r, dn, _ = oenvs[e].step(int(acts[e]))
             ctx = (t, e)
+            assert np.array_equal(vo[e], o), ctx
             assert vr[e] == r, (ctx, vr[e], r)
             assert bool(vd[e]) == dn, ctx
             assert np.array_equal(venv.board[e].cpu().numpy(), oenvs[e].board), ctx
