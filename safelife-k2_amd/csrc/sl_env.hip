@@ -772,25 +772,38 @@ k_env_obs_channels(sl_env_state st, ObsArgs a, uint64_t chpack, uint32_t one,
     const int64_t base = b * n_el * ESZ;                      // first byte
     const int64_t end = base + n_el * ESZ;
     const int64_t c0 = (base + 15) & ~(int64_t)15, c1 = end & ~(int64_t)15;
-    auto elem = [&](int64_t e) -> uint32_t {                  // element e of this env
-        const int cell = (int)(e / nch), k = (int)(e - (int64_t)cell * nch);
+    auto elem = [&](int e) -> uint32_t {                      // element e of this env
+        const int cell = e / nch, k = e - cell * nch;
         return ((vw_[cell] >> ((chpack >> (4 * k)) & 15u)) & 1u) ? one : 0u;
     };
     // partial chunks at both ends (< 16 bytes each): one element per lane
     const int head = (int)(((c0 < end ? c0 : end) - base) / ESZ);
     const int tail = c1 >= c0 ? (int)((end - c1) / ESZ) : 0;
-    int64_t e = -1;
+    int e = -1;                                               // elements per env < 2^16
     if (lane < head) e = lane;
-    else if (lane >= 32 && lane - 32 < tail) e = (c1 - base) / ESZ + (lane - 32);
+    else if (lane >= 32 && lane - 32 < tail) e = (int)((c1 - base) / ESZ) + (lane - 32);
     if (e >= 0) {
         const uint32_t v = elem(e);
         for (int t = 0; t < ESZ; t++) out[base + e * ESZ + t] = (uint8_t)(v >> (8 * t));
     }
-    // whole chunks
-    constexpr int NE = 16 / ESZ;
+    // whole chunks; a lane's next chunk starts 1024 / ESZ elements on, i.e. dcell
+    // cells and dk channels (no division in the loop)
+    constexpr int NE = 16 / ESZ, STEP = 1024 / ESZ;
+    const int dcell = STEP / nch, dk = STEP - dcell * nch;
+    int cell0, k0;
+    {
+        const int e0 = (int)((c0 - base) / ESZ) + lane * NE;
+        cell0 = e0 / nch;
+        k0 = e0 - cell0 * nch;
+    }
     for (int64_t q = c0 + 16 * (int64_t)lane; q < c1; q += 16 * 64) {
-        const int64_t e0 = (q - base) / ESZ;
-        int cell = (int)(e0 / nch), k = (int)(e0 - (int64_t)cell * nch);
+        int cell = cell0, k = k0;
+        cell0 += dcell;
+        k0 += dk;
+        if (k0 >= nch) {
+            k0 -= nch;
+            cell0++;
+        }
         uint32_t v = vw_[cell];
         uint32_t wv[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
