@@ -28,7 +28,8 @@
 // 0 while the column loads are in flight; its cell edits are broadcast and
 // written into the planes before the rule.  Envs that finish are queued; a second
 // kernel (k_env_reset_list) resets exactly those, one wave each, so the step
-// kernel carries no reset code (121 VGPRs, 4 waves/SIMD, no spills).
+// kernel carries no reset code (128 VGPRs, 4 waves/SIMD, no spills).  The <true>
+// instantiation also writes the packed observation (write_obs, 130 VGPRs, 3 waves).
 #include "sl_bits.h"
 
 using namespace sl;

@@ -520,6 +520,33 @@ def test_small_kernel_vs_generic(torch_dev, shape):
         _compare_state(fast, gen, t)
 
 
+@pytest.mark.parametrize("B", [1, 3, 5])
+def test_bitsliced_kernels_tiny_batches(torch_dev, B):
+    """Batches that fill no workgroup: the 64x64 kernel (with fused views and its reset
+    list), the small-board and 128x128 kernels agree with the generic kernel."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    rng = np.random.RandomState(B)
+    pools = [LevelPool.load(os.path.join(GOLDEN, "pools", "c3_prune_still_64.npz")),
+             LevelPool.load(os.path.join(GOLDEN, "pools", "c2_append_still_25.npz")),
+             LevelPool.load(C5_POOL)]
+    for pool in pools:
+        kw = dict(time_limit=9, view_shape=(15, 15), output_channels=None, penalty_coef=1.0,
+                  min_performance=0.01, rng="philox", seed=77, level_order="random",
+                  augment_roll=True)
+        fast = SafeLifeVecEnv(pool, B, "cuda:0", kernel="fast", **kw)
+        gen = SafeLifeVecEnv(pool, B, "cuda:0", kernel="generic", **kw)
+        assert torch.equal(fast.reset(), gen.reset())
+        for t in range(25):
+            a = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+            o1, r1, d1, _ = fast.step(a)
+            o2, r2, d2, _ = gen.step(a)
+            ctx = (pool.H, t)
+            assert torch.equal(r1, r2) and torch.equal(d1, d2), ctx
+            assert torch.equal(o1, o2), ctx
+            _compare_state(fast, gen, ctx)
+
+
 # ------------------------------------------------ 128x128 bit-sliced kernel (C5)
 C5_POOL = os.path.join(GOLDEN, "pools", "c5_navigation_128.npz")
 
