@@ -87,6 +87,11 @@ __device__ __forceinline__ int pm(int a, int m) {
     int r = a % m;
     return r < 0 ? r + m : r;
 }
+// the torus wrap of a coordinate at most one period outside [0, m) (m >= 2: every
+// neighbour offset of the action is within +-2), without a division
+__device__ __forceinline__ int wrap1(int a, int m) {
+    return a < 0 ? a + m : (a >= m ? a - m : a);
+}
 
 // the per-env fields the action reads and writes, straight from sl_env_state
 struct GlobalEnv {
@@ -108,9 +113,12 @@ struct GlobalEnv {
 
 // action a (0..8, safelife_env.py:61-71) on env e; the reward is 1 when the agent
 // walks into an open exit (move_agent, safelife_game.py:356-364), else 0
-template <class Env, class Src>
+// cell (y, x) is overlay index y * S + x, S = STRIDE (0: W); a kernel whose cell
+// source is a padded row image passes the padding stride and decodes indices by shifts
+template <int STRIDE = 0, class Env, class Src>
 __device__ __forceinline__ int act_core(Env &e, int a, int H, int W, int ctp, int ctc,
                                         OverlayT<Src> &ov) {
+    const int S = STRIDE ? STRIDE : W;
     ov.n = 0;
     if (e.game_over() || a < 1 || a > 8) return 0;
     int reward = 0;
@@ -119,10 +127,10 @@ __device__ __forceinline__ int act_core(Env &e, int a, int H, int W, int ctp, in
     const int fx = orient == 1 ? 1 : (orient == 3 ? -1 : 0);
     const int fy = orient == 0 ? -1 : (orient == 2 ? 1 : 0);
     const int x0 = e.agent_x(), y0 = e.agent_y();
-    const int x1 = pm(x0 + fx, W), y1 = pm(y0 + fy, H);
-    const int i0 = y0 * W + x0, i1 = y1 * W + x1;
+    const int x1 = wrap1(x0 + fx, W), y1 = wrap1(y0 + fy, H);
+    const int i0 = y0 * S + x0, i1 = y1 * S + x1;
     if (a <= 4) {
-        const int i2 = pm(y0 - fy, H) * W + pm(x0 - fx, W);
+        const int i2 = wrap1(y0 - fy, H) * S + wrap1(x0 - fx, W);
         int nx = x0, ny = y0;
         const uint32_t c1 = ov.get(i1);
         if (c1 == 0) {
@@ -133,7 +141,7 @@ __device__ __forceinline__ int act_core(Env &e, int a, int H, int W, int ctp, in
             e.set_game_over();
             reward = 1;
         } else if (c1 & PUSHABLE) {
-            const int i3 = pm(y0 + 2 * fy, H) * W + pm(x0 + 2 * fx, W);
+            const int i3 = wrap1(y0 + 2 * fy, H) * S + wrap1(x0 + 2 * fx, W);
             const uint32_t c3 = ov.get(i3);
             if (c3 == 0) {
                 ov.set(i3, ov.get(i1));

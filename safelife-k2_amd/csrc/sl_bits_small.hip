@@ -57,14 +57,12 @@ struct GeoSmall {
 typedef __attribute__((address_space(3))) u32 lds_u32;
 typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
 
-// unedited cells for the action, from the staged board: row y is 32 dwords, cell
-// (y, x) the u16 at y * 64 + x
+// unedited cells for the action, from the staged board: row y is 32 dwords, and the
+// action indexes cell (y, x) as y * 64 + x (act_core<64>)
 struct SmallCells {
     const lds_u32 *buf;
-    int W;
     __device__ __forceinline__ uint32_t operator()(int i) const {
-        const int y = i / W, x = i - y * W;
-        return reinterpret_cast<lds_cu16 *>(buf)[y * 64 + x];
+        return reinterpret_cast<lds_cu16 *>(buf)[i];
     }
 };
 
@@ -120,18 +118,41 @@ __device__ __forceinline__ void lds_rows(const lds_u16 *t, int H, bool active, i
 }
 
 #ifndef SL_SMALL_MINW
-#define SL_SMALL_MINW 3      // waves per SIMD (the 12 KiB LDS stage allows 3.25)
+#define SL_SMALL_MINW 3      // waves per SIMD the register budget is sized for (4 spills
+                             // a few registers and measured no faster)
 #endif
 
+// all kernel arguments in one struct at kernarg offset 0: the epilogue re-reads its
+// ~20 pointers where it runs (kargs()), so they are not held in SGPRs through the step
+struct SmallKArgs {
+    sl_env_state st;
+    StepArgs a;
+    const int32_t *actions;
+    int ctp, ctc;
+    double *reward_out;
+    uint8_t *done_out, *flags_out;
+    int32_t *ep_len_out, *ep_rew_out;
+};
+
+__device__ __forceinline__ const SmallKArgs &kargs() {
+    auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return *(const SmallKArgs *)kp;
+}
+
 __global__ void __launch_bounds__(64, SL_SMALL_MINW)
-k_env_step_small(sl_env_state st, StepArgs a, const int32_t *__restrict__ actions, int ctp,
-                 int ctc, double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
-                 uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
-                 int32_t *__restrict__ ep_rew_out) {
+k_env_step_small(SmallKArgs ka) {
+    const sl_env_state &st = ka.st;
+    const StepArgs &a = ka.a;
+    const int32_t *__restrict__ actions = ka.actions;
+    const int ctp = ka.ctp, ctc = ka.ctc;
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x;
     const int H = st.H, W = st.W, nl = (W + 1) >> 1;
-    __shared__ __attribute__((aligned(16))) u32 stage[3][kMaxH * 32];   // board, goals, start
+    // board, goals, start board: H rows of 32 dwords each (dynamic: 9.4 KiB at 25 rows,
+    // so four waves per SIMD fit the CU's LDS)
+    extern __shared__ __attribute__((aligned(16))) u32 dyn_stage[];
+    u32 *stage[3] = {dyn_stage, dyn_stage + H * 32, dyn_stage + 2 * H * 32};
     lds_u32 *buf = (lds_u32 *)stage[0];
     const bool active = lane < nl;
     const int c0 = 2 * lane, c1 = 2 * lane + 1;             // stores: c1 < W unless odd_last
@@ -193,7 +214,6 @@ k_env_step_small(sl_env_state st, StepArgs a, const int32_t *__restrict__ action
     // ---- board: the action reads the staged cells, then the rows become planes
     OverlayT<SmallCells> ov;
     ov.src.buf = buf;
-    ov.src.W = W;
     ov.n = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -203,16 +223,24 @@ k_env_step_small(sl_env_state st, StepArgs a, const int32_t *__restrict__ action
     RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
                rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     int act_reward = 0;
-    if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), H, W, ctp, ctc, ov);
+    if (lane == 0) act_reward = act_core<64>(env, rec(V, R_ACT), H, W, ctp, ctc, ov);
     act_reward = __builtin_amdgcn_readfirstlane(act_reward);
-    const int ne = __builtin_amdgcn_readfirstlane(ov.n);
-    int eidx[4];
-    u32 eval[4];
+    // the action's cell edits go straight into the staged board (lane 0; the wave's LDS
+    // operations run in order, so the row reads below see them), the column-0 copy of
+    // an odd board too; erow = the rows holding an edit
+    u32 erow = 0;
+    if (lane == 0) {
+        lds_u16 *cells = (lds_u16 *)stage[0];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        eidx[k] = __builtin_amdgcn_readfirstlane(ov.idx[k]);
-        eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
+        for (int k = 0; k < 4; k++)
+            if (k < ov.n) {
+                const int i = ov.idx[k];
+                cells[i] = (uint16_t)ov.val[k];
+                if ((W & 1) && (i & 63) == 0) cells[i + W] = (uint16_t)ov.val[k];
+                erow |= 1u << (i >> 6);
+            }
     }
+    erow = (u32)__builtin_amdgcn_readfirstlane((int)erow);
     RecFields fl{V, __builtin_amdgcn_readfirstlane(env.go), __builtin_amdgcn_readfirstlane(env.ax),
                  __builtin_amdgcn_readfirstlane(env.ay), 0.0};
     if (a.bonus_period > 0)
@@ -221,24 +249,6 @@ k_env_step_small(sl_env_state st, StepArgs a, const int32_t *__restrict__ action
                                            a.bonus_period, a.bonus_len)];
     lds_rows((const lds_u16 *)stage[0], H, active, lane, PB);
     transpose32(PB);
-    u32 erow = 0;                              // rows holding an edit
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        if (k < ne) {
-            const int y = eidx[k] / W, x = eidx[k] - (eidx[k] / W) * W;
-            const u32 bit = 1u << y;
-            // the cell's word, and for x = 0 with odd W also the last lane's copy
-            const u32 m0 = (lane == (x >> 1) && !(x & 1)) ? bit : 0u;
-            const u32 m1 = ((lane == (x >> 1) && (x & 1)) || (x == 0 && geo.odd_last)) ? bit : 0u;
-            erow |= bit;
-#pragma unroll
-            for (int p = 0; p < 16; p++) {
-                const u32 v = ((eval[k] >> p) & 1u) ? ~0u : 0u;
-                PL(PB, p, 0) = mux(m0, v, PL(PB, p, 0));
-                PL(PB, p, 1) = mux(m1, v, PL(PB, p, 1));
-            }
-        }
-    }
     u32 cb[2];
     rule_planes(PB, cb, geo, sc, 0u);
     __builtin_amdgcn_sched_barrier(0);
@@ -280,9 +290,11 @@ k_env_step_small(sl_env_state st, StepArgs a, const int32_t *__restrict__ action
                 if (!geo.odd_last) gb[y * W + c1] = (uint16_t)(PB[y] >> 16);
             }
     }
-    if (lane == 0)
-        epilogue_core(st, a, b, fl, act_reward, points, score, possible, side_total, reward_out,
-                      done_out, flags_out, ep_len_out, ep_rew_out);
+    if (lane == 0) {
+        const SmallKArgs &k = kargs();
+        epilogue_core(k.st, k.a, b, fl, act_reward, points, score, possible, side_total,
+                      k.reward_out, k.done_out, k.flags_out, k.ep_len_out, k.ep_rew_out);
+    }
 }
 
 }  // namespace
@@ -298,8 +310,9 @@ int launch_step_small(const sl_env_state &st, const StepArgs &a, const int32_t *
                       int32_t *ep_rew, hipStream_t s) {
     if (!small_shape(st)) return SL_ETOOBIG;
     if (st.B > 0x7FFFFFFF) return SL_EINVAL;
-    hipLaunchKernelGGL(k_env_step_small, dim3((unsigned)st.B), dim3(64), 0, s, st, a, actions, ctp,
-                       ctc, reward, done, flags, ep_len, ep_rew);
+    const SmallKArgs ka{st, a, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
+    const size_t lds = (size_t)3 * st.H * 32 * sizeof(uint32_t);
+    hipLaunchKernelGGL(k_env_step_small, dim3((unsigned)st.B), dim3(64), lds, s, ka);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
