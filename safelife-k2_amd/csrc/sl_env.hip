@@ -745,16 +745,21 @@ k_env_obs_packed_list(sl_env_state st, ObsArgs a, uint16_t *__restrict__ out,
         obs_packed_wave(st, a, __builtin_amdgcn_readfirstlane(list[i]), threadIdx.x & 63, out);
 }
 
-// channel obs: the view is gathered into the wave's LDS buffer, then the env's
-// output bytes [b R, (b+1) R) are written as 16-byte vectors where they cover a
-// whole aligned chunk (R = 32 670 B at 33x33x15 u16 is only 2-byte aligned, so the
-// partial chunks at both ends are written element by element).  ESZ = element
-// bytes; channel k of a cell is bit (chpack >> 4k) & 15 of its value.
+// channel obs.  Per view cell the wave first stores in LDS the cell's CHANNEL MASK
+// m = sum_k bit(v, ch[k]) << k (one AND for the usual channels 0..nch-1); output
+// element e = (cell, k) is then bit k of m[cell].  The env's output bytes
+// [b R, (b+1) R) are written as 16-byte vectors where they cover a whole aligned
+// chunk (R = 32 670 B at 33x33x15 u16 is only 2-byte aligned, so the partial chunks
+// at both ends are written element by element).  A chunk's 16 / ESZ element bits are
+// gathered from one to three masks and expanded to bytes / halfwords / words by a
+// multiply-and-mask spread (no per-element shifts or selects).  ESZ = element bytes;
+// `one` = the element's 1 (1, 0x3F80 bf16, 0x3F800000 f32).  LDS: 4 views per
+// workgroup, sized by the launch (vpad cells each).
 template <int ESZ>
 __global__ void __launch_bounds__(256)
-k_env_obs_channels(sl_env_state st, ObsArgs a, uint64_t chpack, uint32_t one,
+k_env_obs_channels(sl_env_state st, ObsArgs a, uint64_t chpack, uint32_t one, int vpad,
                    uint8_t *__restrict__ out) {
-    __shared__ uint16_t view[4][kObsMaxCells];
+    extern __shared__ __attribute__((aligned(16))) uint16_t obs_lds[];
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int64_t b = (int64_t)blockIdx.x * 4 + wid;
     const int lane = threadIdx.x & 63;
@@ -762,20 +767,27 @@ k_env_obs_channels(sl_env_state st, ObsArgs a, uint64_t chpack, uint32_t one,
     ObsWave w;
     obs_wave_init(st, a, b, w);
     const int nv = a.vh * a.vw, nch = a.nch;
-    uint16_t *vw_ = view[wid];
+    uint16_t *vw_ = obs_lds + wid * vpad;
+    // channels 0..nch-1 in order: the mask is the value's low bits
+    bool ident = true;
+    for (int k = 0; k < nch; k++) ident = ident && ((chpack >> (4 * k)) & 15u) == (uint64_t)k;
+    const uint32_t lowmask = (1u << nch) - 1u;
     int i0 = lane, r = lane / a.vw, c = lane - (lane / a.vw) * a.vw;
     while (i0 < nv)
-        obs_wave_cells(st, a, w, nv, i0, r, c, [&](int i, uint32_t v) { vw_[i] = (uint16_t)v; });
+        obs_wave_cells(st, a, w, nv, i0, r, c, [&](int i, uint32_t v) {
+            uint32_t m = v & lowmask;
+            if (!ident) {
+                m = 0u;
+                for (int k = 0; k < nch; k++) m |= ((v >> ((chpack >> (4 * k)) & 15u)) & 1u) << k;
+            }
+            vw_[i] = (uint16_t)m;
+        });
     // LDS operations of one wave complete in order: the reads below see the writes
     __builtin_amdgcn_wave_barrier();
     const int64_t n_el = (int64_t)nv * nch;                  // elements per env
     const int64_t base = b * n_el * ESZ;                      // first byte
     const int64_t end = base + n_el * ESZ;
     const int64_t c0 = (base + 15) & ~(int64_t)15, c1 = end & ~(int64_t)15;
-    auto elem = [&](int e) -> uint32_t {                      // element e of this env
-        const int cell = e / nch, k = e - cell * nch;
-        return ((vw_[cell] >> ((chpack >> (4 * k)) & 15u)) & 1u) ? one : 0u;
-    };
     // partial chunks at both ends (< 16 bytes each): one element per lane
     const int head = (int)(((c0 < end ? c0 : end) - base) / ESZ);
     const int tail = c1 >= c0 ? (int)((end - c1) / ESZ) : 0;
@@ -783,7 +795,8 @@ k_env_obs_channels(sl_env_state st, ObsArgs a, uint64_t chpack, uint32_t one,
     if (lane < head) e = lane;
     else if (lane >= 32 && lane - 32 < tail) e = (int)((c1 - base) / ESZ) + (lane - 32);
     if (e >= 0) {
-        const uint32_t v = elem(e);
+        const int cell = e / nch, k = e - cell * nch;
+        const uint32_t v = ((vw_[cell] >> k) & 1u) ? one : 0u;
         for (int t = 0; t < ESZ; t++) out[base + e * ESZ + t] = (uint8_t)(v >> (8 * t));
     }
     // whole chunks; a lane's next chunk starts 1024 / ESZ elements on, i.e. dcell
@@ -797,24 +810,28 @@ k_env_obs_channels(sl_env_state st, ObsArgs a, uint64_t chpack, uint32_t one,
         k0 = e0 - cell0 * nch;
     }
     for (int64_t q = c0 + 16 * (int64_t)lane; q < c1; q += 16 * 64) {
-        int cell = cell0, k = k0;
+        // the chunk's NE element bits, low bit first
+        uint32_t bits = (uint32_t)vw_[cell0] >> k0;
+        int have = nch - k0, cn = cell0 + 1;
+        while (have < NE) {
+            bits |= (uint32_t)vw_[cn++] << have;
+            have += nch;
+        }
         cell0 += dcell;
         k0 += dk;
         if (k0 >= nch) {
             k0 -= nch;
             cell0++;
         }
-        uint32_t v = vw_[cell];
-        uint32_t wv[4] = {0u, 0u, 0u, 0u};
+        uint32_t wv[4];
 #pragma unroll
-        for (int t = 0; t < NE; t++) {
-            const uint32_t bit = (v >> ((chpack >> (4 * k)) & 15u)) & 1u;
-            wv[(t * ESZ) >> 2] |= (bit ? one : 0u) << (((t * ESZ) & 3) * 8);
-            if (++k == nch) {
-                k = 0;
-                ++cell;
-                if (t + 1 < NE) v = vw_[cell];
-            }
+        for (int j = 0; j < 4; j++) {
+            if (ESZ == 1)        // 4 bits -> 4 bytes
+                wv[j] = ((((bits >> (4 * j)) & 15u) * 0x00204081u) & 0x01010101u) * one;
+            else if (ESZ == 2)   // 2 bits -> 2 halfwords
+                wv[j] = ((((bits >> (2 * j)) & 3u) * 0x8001u) & 0x00010001u) * one;
+            else                 // 1 bit -> 1 word
+                wv[j] = ((bits >> j) & 1u) * one;
         }
         *reinterpret_cast<uint4 *>(out + q) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     }
@@ -881,12 +898,18 @@ int launch_obs(const sl_env_state &st, const ObsArgs &a, void *out, hipStream_t 
                              : a.mode == SL_OBS_CHANNELS_BF16 ? 0x3F80u : 1u;
         const dim3 grid((unsigned)((st.B + 3) / 4));
         uint8_t *o = (uint8_t *)out;
+        // + 2 cells: a chunk's bit gather may read up to two masks past the last cell
+        const int vpad = (nv + 2 + 7) & ~7;
+        const size_t lds = (size_t)4 * vpad * sizeof(uint16_t);
         if (a.mode == SL_OBS_CHANNELS_U8)
-            hipLaunchKernelGGL(k_env_obs_channels<1>, grid, dim3(256), 0, s, st, a, chpack, one, o);
+            hipLaunchKernelGGL(k_env_obs_channels<1>, grid, dim3(256), lds, s, st, a, chpack, one,
+                               vpad, o);
         else if (a.mode == SL_OBS_CHANNELS_F32)
-            hipLaunchKernelGGL(k_env_obs_channels<4>, grid, dim3(256), 0, s, st, a, chpack, one, o);
+            hipLaunchKernelGGL(k_env_obs_channels<4>, grid, dim3(256), lds, s, st, a, chpack, one,
+                               vpad, o);
         else
-            hipLaunchKernelGGL(k_env_obs_channels<2>, grid, dim3(256), 0, s, st, a, chpack, one, o);
+            hipLaunchKernelGGL(k_env_obs_channels<2>, grid, dim3(256), lds, s, st, a, chpack, one,
+                               vpad, o);
         return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
     }
     // unaligned output or a large view: the LDS-staged kernel, one workgroup per env

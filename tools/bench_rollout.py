@@ -43,8 +43,12 @@ def main():
 
     T = args.steps_per_env
     values = torch.zeros((T + 1, args.envs, 1), dtype=torch.float32, device=dev)
-    ro = run_agents(venv, policy, T)          # warm-up (includes the first reset)
-    returns_advantages(ro.rewards, ro.end_episode, values)
+    # warm-up: the first reset, and both rollout buffers the loop keeps alive (the
+    # previous Rollout is still referenced while the next is allocated; a fresh
+    # multi-GB device allocation costs ~0.5 s and is not part of a rollout)
+    for _ in range(2):
+        ro = run_agents(venv, policy, T)
+        returns_advantages(ro.rewards, ro.end_episode, values)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.rollouts):
