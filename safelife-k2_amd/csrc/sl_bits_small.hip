@@ -132,12 +132,101 @@ struct SmallKArgs {
     double *reward_out;
     uint8_t *done_out, *flags_out;
     int32_t *ep_len_out, *ep_rew_out;
+    sl_level_pool pool;       // auto-reset source (K == 0: no reset here)
+    ResetArgs ra;
 };
 
 __device__ __forceinline__ const SmallKArgs &kargs() {
     auto kp = __builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(kp));
     return *(const SmallKArgs *)kp;
+}
+
+// SafeLifeEnv.reset (safelife_env.py:188-198) of env b by its own wave, right after
+// the step that ended the episode (ContinuingEnv + run_agents' reset-on-done): the
+// same result as reset_one (sl_env.hip).  Pass 1 sums points / baseline / possible
+// over the level (a roll permutes cells, so the level's own order is used) and lists
+// the exits of the ROLLED board in np.nonzero order (row-major chunks of 64 cells, a
+// ballot prefix count within a chunk); pass 2 copies the rolled level into board
+// (exits coloured), goals and start board.
+__device__ __forceinline__ void small_reset(const sl_env_state &st, const sl_level_pool &pool,
+                                            const ResetArgs &ra, int64_t b, int lane) {
+    const int H = st.H, W = st.W, hw = H * W;
+    int li = 0, dy = 0, dx = 0;
+    if (lane == 0) {
+        const LevelChoice c = choose_level(pool, ra, ra.env0 + (uint32_t)b, st.episodes[b], H, W);
+        li = c.idx;
+        dy = c.dy;
+        dx = c.dx;
+    }
+    li = __builtin_amdgcn_readfirstlane(li);
+    dy = __builtin_amdgcn_readfirstlane(dy);
+    dx = __builtin_amdgcn_readfirstlane(dx);
+    const uint16_t *lb = pool.board + (int64_t)li * hw, *lg = pool.goals + (int64_t)li * hw;
+    const int dy64 = 64 / W, dx64 = 64 - dy64 * W;
+    const uint64_t below = (1ull << lane) - 1ull;
+    int p = 0, q = 0, r = 0, spb = 0, n_exit = 0;
+    {
+        int y = lane / W, x = lane - (lane / W) * W;
+        for (int i0 = 0; i0 < hw; i0 += 64) {
+            const int i = i0 + lane;
+            bool ex = false;
+            if (i < hw) {
+                const int src = wrap1(y - dy, H) * W + wrap1(x - dx, W);
+                const uint32_t vb = lb[src], vg = lg[src];
+                int pp, qq, rr;
+                cell_scores(vb, vg, &pp, &qq, &rr);
+                p += pp;
+                q += qq;
+                r += rr;
+                spb |= ((vb & SPAWN) ? 1 : 0) | ((vg & SPAWN) ? 2 : 0);
+                ex = (vb & EXIT) != 0;
+            }
+            const uint64_t m = __ballot(ex);
+            const int rank = __builtin_popcountll(m & below);
+            if (ex && n_exit + rank < SL_MAX_EXITS) {
+                st.exit_y[b * SL_MAX_EXITS + n_exit + rank] = (int16_t)y;
+                st.exit_x[b * SL_MAX_EXITS + n_exit + rank] = (int16_t)x;
+            }
+            n_exit += __builtin_popcountll(m);
+            y += dy64;
+            x += dx64;
+            if (x >= W) {
+                x -= W;
+                y++;
+            }
+        }
+    }
+    p = wave_total(p);
+    q = wave_total(q);
+    r = wave_total(r);
+    spb = (int)wave_or((u32)spb);
+    int ev = 0;
+    if (lane == 0) {
+        ev = reset_scalars(st, pool, ra, b, li, dy, dx, p, q, r, spb);
+        st.exit_count[b] = n_exit;
+        for (int e = n_exit; e < SL_MAX_EXITS; e++) {
+            st.exit_y[b * SL_MAX_EXITS + e] = 0;
+            st.exit_x[b * SL_MAX_EXITS + e] = 0;
+        }
+    }
+    ev = __builtin_amdgcn_readfirstlane(ev);
+    const int64_t off = b * (int64_t)hw;
+    uint16_t *gb = st.board + off, *gg = st.goals + off, *gs = st.start_board + off;
+    int y = lane / W, x = lane - (lane / W) * W;
+    for (int i = lane; i < hw; i += 64) {
+        const int src = wrap1(y - dy, H) * W + wrap1(x - dx, W);
+        const uint16_t vb = lb[src];
+        gs[i] = vb;
+        gb[i] = (vb & EXIT) ? (uint16_t)ev : vb;
+        gg[i] = lg[src];
+        y += dy64;
+        x += dx64;
+        if (x >= W) {
+            x -= W;
+            y++;
+        }
+    }
 }
 
 __global__ void __launch_bounds__(64, SL_SMALL_MINW)
@@ -290,10 +379,20 @@ k_env_step_small(SmallKArgs ka) {
                 if (!geo.odd_last) gb[y * W + c1] = (uint16_t)(PB[y] >> 16);
             }
     }
+    int rs = 0;
     if (lane == 0) {
         const SmallKArgs &k = kargs();
-        epilogue_core(k.st, k.a, b, fl, act_reward, points, score, possible, side_total,
-                      k.reward_out, k.done_out, k.flags_out, k.ep_len_out, k.ep_rew_out);
+        rs = epilogue_core(k.st, k.a, b, fl, act_reward, points, score, possible, side_total,
+                           k.reward_out, k.done_out, k.flags_out, k.ep_len_out, k.ep_rew_out)
+                 ? 1 : 0;
+    }
+    rs = __builtin_amdgcn_readfirstlane(rs);
+    if (rs) {
+        const SmallKArgs &k = kargs();
+        if (k.pool.K > 0) {
+            wait_vm();         // this step's stores to the env have completed
+            small_reset(k.st, k.pool, k.ra, b, lane);
+        }
     }
 }
 
@@ -305,12 +404,15 @@ bool small_shape(const sl_env_state &st) {
     return st.H >= 2 && st.H <= kMaxH && st.W >= 2 && st.W <= kMaxW;
 }
 
-int launch_step_small(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
-                      int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
-                      int32_t *ep_rew, hipStream_t s) {
+int launch_step_small(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
+                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
+                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (!small_shape(st)) return SL_ETOOBIG;
     if (st.B > 0x7FFFFFFF) return SL_EINVAL;
-    const SmallKArgs ka{st, a, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
+    sl_level_pool pool = fx.pool;
+    if (!fx.fuse_reset || pool.H != st.H || pool.W != st.W) pool.K = 0;
+    const SmallKArgs ka{st, a, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew, pool,
+                        fx.ra};
     const size_t lds = (size_t)3 * st.H * 32 * sizeof(uint32_t);
     hipLaunchKernelGGL(k_env_step_small, dim3((unsigned)st.B), dim3(64), lds, s, ka);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;

@@ -1057,9 +1057,11 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         reset_done = fx.fuse_reset && fx.pool.K > 0;
     } else if (small) {
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
-        int rc = launch_step_small(*st, a, actions, cfg->can_toggle_powers, cfg->can_toggle_colors,
-                                   reward, done, info_flags, ep_len, ep_reward, s);
+        int rc = launch_step_small(*st, a, fx, actions, cfg->can_toggle_powers,
+                                   cfg->can_toggle_colors, reward, done, info_flags, ep_len,
+                                   ep_reward, s);
         if (rc) return rc;
+        reset_done = fx.fuse_reset && fx.pool.K > 0 && fx.pool.H == st->H && fx.pool.W == st->W;
     } else if (fast) {
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
         int rc = launch_step_fast(*st, a, fx, actions, cfg->can_toggle_powers,

@@ -261,9 +261,10 @@ bool launch_fast_fuses_obs();
 bool bits128_shape(const sl_env_state &st);
 // the bit-sliced kernel for boards up to 32 x 64 (sl_bits_small.hip)
 bool small_shape(const sl_env_state &st);
-int launch_step_small(const sl_env_state &st, const StepArgs &a, const int32_t *actions, int ctp,
-                      int ctc, double *reward, uint8_t *done, uint8_t *flags, int32_t *ep_len,
-                      int32_t *ep_rew, hipStream_t s);
+// (auto-reset: envs whose episode ended are reset by their own wave from fx.pool)
+int launch_step_small(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
+                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
+                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
 int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                         const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                         uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
