@@ -63,15 +63,17 @@ __device__ unsigned long long g_sl_phase128[1024][12];
 // Tuning switches; the defaults are the measured best on C5 (MI355X, bench_variants):
 //   PF=1 (next band's rows loaded a band ahead, stores issued behind them): no gain,
 //     the start-board loads queue behind the prefetch (vmcnt is in order);
-//   NOPOOL=0 (start board from the pool's bit planes, 44 cache-resident dword loads
-//     per band): 32.9 vs 37.1 M env-steps/s for NOPOOL=1 (32 HBM loads + transpose);
+//   NOPOOL=0 (start board from the pool's bit planes, DMA'd into LDS at the band's
+//     start, read after the rule): 43.9 vs 38.6 M env-steps/s for NOPOOL=1 (32 HBM
+//     loads + transpose; same box).  Gathering the planes straight from L2 into
+//     registers instead (held across the rule) measured 32.9 vs 37.1;
 //   SEARLY=1: the start board's rows are issued right behind the band's rows, so
 //     they are in flight under the rule.
 #ifndef SL_B128_PF
 #define SL_B128_PF 0
 #endif
 #ifndef SL_B128_NOPOOL
-#define SL_B128_NOPOOL 1
+#define SL_B128_NOPOOL 0
 #endif
 #ifndef SL_B128_SEARLY
 #define SL_B128_SEARLY 1
@@ -173,25 +175,44 @@ __device__ __forceinline__ u32 edit_row(u32 d, int r, int ne, const int eidx[4],
     return d;
 }
 
-// The start board's planes for band t from the level pool's bit planes
-// (sl_level_pool.board_planes, [p][q][x] words of one level): the env's start board
-// is the level rolled by (dy, dx), so column c is level column c - dx and band row y
-// is level row 32t + y - dy, one funnel shift of two adjacent 32-row words.  Only
-// the planes the side-effect term reads are fetched; the pool stays in L2 / MALL.
-__device__ __forceinline__ void pool_start(const u32 *__restrict__ pp, int t, int dy, int c0,
-                                           int c1, u32 S[32]) {
+// The start-board planes the side-effect term reads (0, 2, 7-15), from the level
+// pool's bit planes when the env was reset from the pool (SL_B128_NOPOOL=0): row y of
+// band t is level row 32t + y - dy, one funnel shift of two adjacent 32-row words;
+// column c is level column c - dx.  At a band's
+// start one global_load_lds per plane copies the two level bands it spans (lanes
+// 0-31: band q0, lanes 32-63: band q1, 128 columns each) into the wave's 11 KiB
+// buffer, so the copy runs under the band's rule and holds no registers; after the
+// rule each word is two LDS reads and a funnel shift.
+constexpr int kPoolPlanes = 11;      // planes 0, 2, 7-15
+__device__ __forceinline__ int pool_plane(int s) { return s == 0 ? 0 : (s == 1 ? 2 : s + 5); }
+
+__device__ __forceinline__ void pool_dma128(const u32 *__restrict__ pp, int t, int dy, int lane,
+                                            __attribute__((address_space(3))) u32 *buf) {
     const int r0 = (32 * t - dy) & (N - 1), q0 = r0 >> 5, q1 = (q0 + 1) & (NB - 1);
-    const u32 sh = (u32)(r0 & 31);
+    const int qq = lane < 32 ? q0 : q1;
+#pragma unroll
+    for (int s = 0; s < kPoolPlanes; s++) {
+        const u32 *src = pp + (pool_plane(s) * NB + qq) * N + 4 * (lane & 31);
+        __builtin_amdgcn_global_load_lds((const void *)src,
+                                         (__attribute__((address_space(3))) void *)(buf + s * 256),
+                                         16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void pool_start_lds(const __attribute__((address_space(3))) u32 *buf,
+                                               int t, int dy, int c0, int c1, u32 S[32]) {
+    const u32 sh = (u32)((32 * t - dy) & 31);
 #pragma unroll
     for (int p = 0; p < 16; p++) {
-        if (p == 1 || (p >= 3 && p <= 6)) {
-            PL(S, p, 0) = 0u;
-            PL(S, p, 1) = 0u;
-            continue;
-        }
-        const u32 *lo = pp + (p * NB + q0) * N, *hi = pp + (p * NB + q1) * N;
-        PL(S, p, 0) = __builtin_amdgcn_alignbit(hi[c0], lo[c0], sh);
-        PL(S, p, 1) = __builtin_amdgcn_alignbit(hi[c1], lo[c1], sh);
+        PL(S, p, 0) = 0u;
+        PL(S, p, 1) = 0u;
+    }
+#pragma unroll
+    for (int s = 0; s < kPoolPlanes; s++) {
+        const int p = pool_plane(s);
+        const __attribute__((address_space(3))) u32 *q = buf + s * 256;
+        PL(S, p, 0) = __builtin_amdgcn_alignbit(q[128 + c0], q[c0], sh);
+        PL(S, p, 1) = __builtin_amdgcn_alignbit(q[128 + c1], q[c1], sh);
     }
 }
 
@@ -215,6 +236,10 @@ k_env_step_bits128(sl_env_state st, StepArgs a, FastExtra fx,
     TM_SET(0);
     const u32 V = load_record(st, actions, b, lane);
     __shared__ uint16_t draw_list[64 * 64];
+#if !SL_B128_NOPOOL
+    __shared__ __attribute__((aligned(16))) u32 spool_[kPoolPlanes * 256];
+    __attribute__((address_space(3))) u32 *spool = (__attribute__((address_space(3))) u32 *)spool_;
+#endif
     __shared__ u32 draw_res[128], draw_cnt;
     const DrawLds dl{(lds_u16_t *)draw_list, (lds_u32_t *)draw_res, (lds_u32_t *)&draw_cnt};
     // pre-step halo rows of every band: above (32t - 1) and below (32t + 32)
@@ -340,7 +365,12 @@ k_env_step_bits128(sl_env_state st, StepArgs a, FastExtra fx,
             load_pairs<RS>(gb + 32 * t * RS, P);
             if (SL_B128_SEARLY && roll < 0 && !(SL_B128_ABL & 1)) load_pairs<RS>(gs + 32 * t * RS, S);
         }
-        if (roll >= 0 && !(SL_B128_ABL & 1)) pool_start(pp, t, sdy, sc0, sc1, S);
+#if !SL_B128_NOPOOL
+        if (roll >= 0 && !(SL_B128_ABL & 1)) {
+            wait_lgkm();        // the previous band's reads of the buffer are done
+            pool_dma128(pp, t, sdy, lane, spool);
+        }
+#endif
         transpose32(P);
         const u32 erow = apply_edits(P, ne, eidx, eval, 32 * t, lane);
         TM_ACC(4);
@@ -360,6 +390,11 @@ k_env_step_bits128(sl_env_state st, StepArgs a, FastExtra fx,
         } else if (roll < 0) {
             if (!(SL_B128_SEARLY && !SL_B128_PF)) load_pairs<RS>(gs + 32 * t * RS, S);
             transpose32(S);
+        } else {
+#if !SL_B128_NOPOOL
+            wait_vm();          // the band's pool planes have landed in LDS
+            pool_start_lds(spool, t, sdy, sc0, sc1, S);
+#endif
         }
         TM_ACC(6);
         u32 gcol[3][2];
