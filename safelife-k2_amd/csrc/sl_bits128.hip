@@ -216,12 +216,32 @@ __device__ __forceinline__ void pool_start_lds(const __attribute__((address_spac
     }
 }
 
+// all kernel arguments in one struct at kernarg offset 0: the epilogue re-reads its
+// pointers where it runs (kargs128()), so they are not held in SGPRs through the bands
+struct Step128KArgs {
+    sl_env_state st;
+    StepArgs a;
+    FastExtra fx;
+    const int32_t *actions;
+    int ctp, ctc;
+    double *reward_out;
+    uint8_t *done_out, *flags_out;
+    int32_t *ep_len_out, *ep_rew_out;
+};
+
+__device__ __forceinline__ const Step128KArgs &kargs128() {
+    auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return *(const Step128KArgs *)kp;
+}
+
 __global__ void __launch_bounds__(64, SL_B128_MINW)
-k_env_step_bits128(sl_env_state st, StepArgs a, FastExtra fx,
-                   const int32_t *__restrict__ actions, int ctp,
-                   int ctc, double *__restrict__ reward_out, uint8_t *__restrict__ done_out,
-                   uint8_t *__restrict__ flags_out, int32_t *__restrict__ ep_len_out,
-                   int32_t *__restrict__ ep_rew_out) {
+k_env_step_bits128(Step128KArgs ka) {
+    const sl_env_state &st = ka.st;
+    const StepArgs &a = ka.a;
+    const FastExtra &fx = ka.fx;
+    const int32_t *__restrict__ actions = ka.actions;
+    const int ctp = ka.ctp, ctc = ka.ctc;
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x;
     const int64_t off = b * (int64_t)(N * N);
@@ -437,13 +457,14 @@ k_env_step_bits128(sl_env_state st, StepArgs a, FastExtra fx,
     wait_vm();              // row stores land before the epilogue rewrites the exits
     TM_SET(9);
     if (lane == 0) {
-        const bool reset = epilogue_core(st, a, b, fl, act_reward, points, score, possible,
-                                         side_total, reward_out, done_out, flags_out, ep_len_out,
-                                         ep_rew_out);
-        if (fx.fuse_reset && reset) {   // queued for k_env_reset_list_wide
-            int64_t *cnt = fx.scratch + 8 * st.B + 2 + (a.step & 1);
+        const Step128KArgs &k = kargs128();
+        const bool reset = epilogue_core(k.st, k.a, b, fl, act_reward, points, score, possible,
+                                         side_total, k.reward_out, k.done_out, k.flags_out,
+                                         k.ep_len_out, k.ep_rew_out);
+        if (k.fx.fuse_reset && reset) {   // queued for k_env_reset_list_wide
+            int64_t *cnt = k.fx.scratch + 8 * k.st.B + 2 + (k.a.step & 1);
             const int i = (int)atomicAdd((unsigned long long *)cnt, 1ull);
-            reinterpret_cast<int32_t *>(fx.scratch + 2 * st.B)[i] = (int32_t)b;
+            reinterpret_cast<int32_t *>(k.fx.scratch + 2 * k.st.B)[i] = (int32_t)b;
         }
     }
 #if SL_B128_TIMING
@@ -472,8 +493,8 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
                         const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                         uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (!bits128_shape(st)) return SL_ETOOBIG;
-    hipLaunchKernelGGL(k_env_step_bits128, dim3((unsigned)st.B), dim3(64), 0, s, st, a, fx,
-                       actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
+    const Step128KArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
+    hipLaunchKernelGGL(k_env_step_bits128, dim3((unsigned)st.B), dim3(64), 0, s, ka);
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.fuse_reset && fx.pool.K > 0)
         return launch_reset_list_wide(st, fx.pool, fx.ra, fx.scratch, a.step, s);
