@@ -31,6 +31,7 @@
 // kernel carries no reset code (128 VGPRs, 4 waves/SIMD, no spills).  The <true>
 // instantiation also writes the packed observation (write_obs, 130 VGPRs, 3 waves).
 #include "sl_bits.h"
+#include "sl_obs.h"
 
 using namespace sl;
 using namespace sl::fast;
@@ -330,7 +331,7 @@ __device__ __forceinline__ const StepKArgs &kernarg() {
 // HBM store) and the view-form rows, which go to the wave's LDS buffer in dma_board's
 // layout; a board with any of those bits set takes a bit-sliced add and two more
 // transposes instead.  Each view cell is then one u16 LDS read.  Envs reset after the
-// step get their view rewritten by k_env_obs_packed_list.
+// step get their view written by the reset-list kernel after their reset.
 __device__ __forceinline__ void lds_put_board(lds_u32 *buf, int lane, const u32 D[32]) {
     const int h = lane & 1, j = lane >> 1;
     lds_u32 *p = buf + h * 1024 + ((j + 16 * h) & 31);
@@ -708,15 +709,24 @@ k_env_step_bits64(StepKArgs ka) {
 
 // Resets the envs the step kernel queued (one wave per env, grid-stride over the
 // list).  Also zeroes the other step parity's list length for the next step.
+// With obs_out, each reset env's packed view is then written from the new episode
+// (the step kernel wrote the views of all other envs).
 __global__ void __launch_bounds__(64)
 k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scratch,
-                 uint32_t step) {
+                 uint32_t step, sl::obs::ObsArgs oa, uint16_t *obs_out) {
     int64_t *cnt = scratch + 8 * st.B + 2;
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(step + 1) & 1] = 0;
     const int n = (int)__builtin_amdgcn_readfirstlane((int)cnt[step & 1]);
     const int32_t *list = reinterpret_cast<const int32_t *>(scratch + 2 * st.B);
-    for (int i = blockIdx.x; i < n; i += gridDim.x)
-        wave_reset(st, pool, ra, __builtin_amdgcn_readfirstlane(list[i]), threadIdx.x);
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int64_t b = __builtin_amdgcn_readfirstlane(list[i]);
+        wave_reset(st, pool, ra, b, threadIdx.x);
+        if (obs_out) {
+            wait_vm();      // the reset's stores have landed (no stale lines: this wave
+                            // alone touches env b, and L1 starts clean each launch)
+            sl::obs::obs_packed_wave(st, oa, b, threadIdx.x, obs_out);
+        }
+    }
 }
 
 }  // namespace
@@ -751,8 +761,14 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.fuse_reset && fx.pool.K > 0) {
         const unsigned grid = (unsigned)(st.B < 512 ? st.B : 512);
+        sl::obs::ObsArgs oa{};
+        oa.vh = fx.obs_vh;
+        oa.vw = fx.obs_vw;
+        oa.remove_white = fx.obs_rw;
+        oa.mode = SL_OBS_PACKED;
+        oa.nch = 0;
         hipLaunchKernelGGL(k_env_reset_list, dim3(grid), dim3(64), 0, s, st, fx.pool, fx.ra,
-                           fx.scratch, a.step);
+                           fx.scratch, a.step, oa, fx.obs_out);
     }
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }

@@ -14,10 +14,12 @@
 //   k_env_obs         get_obs + recenter_view (safelife_env.py:125-155,
 //                     helper_utils.py:41-74)
 #include "sl_env_common.h"
+#include "sl_obs.h"
 
 #include <math.h>
 
 using namespace sl;
+using namespace sl::obs;
 
 namespace {
 
@@ -571,17 +573,6 @@ k_env_reset_scan(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict_
 // ---------------------------------------------------------------------------
 // observations
 // ---------------------------------------------------------------------------
-struct ObsArgs {
-    int vh, vw, remove_white, mode, nch;
-    int ch[16];
-};
-
-__device__ __forceinline__ uint16_t obs_value(uint32_t bv, uint32_t gv, int remove_white) {
-    uint32_t g = gv & COLORS;
-    if (remove_white && g == COLORS) g = 0;
-    return (uint16_t)((bv + (g << 3)) & 0xFFFFu);
-}
-
 // channel k of cell i = bit a.ch[k] of view[i], stored as the pattern 0 / `one` of an
 // element type of T's width (0/1 integers, or 0.0/1.0 as float32 / bfloat16 -- the
 // policy's layer0, training/safelife_ppo.py:147-152, without a separate cast pass)
@@ -635,114 +626,11 @@ k_env_obs(sl_env_state st, ObsArgs a, void *__restrict__ out) {
     }
 }
 
-// ---- wave-per-env observation kernels ---------------------------------------
-// One wave per env, four per workgroup, no block barrier.  Lane l handles the view
-// cells i = l + 64k (flat row-major order).  The cells' board and goals loads are
-// issued eight at a time, all independent, so a wave keeps 16 gathers in flight.
-// Exits are moved onto their clipped position on the view (recenter_view,
-// helper_utils.py:55-72); the targets and values are wave-uniform and computed up
-// front; the last exit in np.nonzero order wins a shared target.
-constexpr int kObsGroup = 8;
-constexpr int kObsMaxCells = 4096;        // view cells handled by the wave kernels
-
-struct ObsWave {
-    const uint16_t *gb, *gg;
-    int ty, tx, ne;
-    int tgt[SL_MAX_EXITS];
-    uint32_t val[SL_MAX_EXITS];
-};
-
-__device__ __forceinline__ void obs_wave_init(const sl_env_state &st, const ObsArgs &a, int64_t b,
-                                              ObsWave &w) {
-    const int H = st.H, W = st.W;
-    const int64_t hw = (int64_t)H * W;
-    w.gb = st.board + b * hw;
-    w.gg = st.goals + b * hw;
-    const int y0 = st.agent_y[b], x0 = st.agent_x[b];
-    w.ty = y0 - a.vh / 2;
-    w.tx = x0 - a.vw / 2;
-    w.ne = min(st.exit_count[b], SL_MAX_EXITS);
-#pragma unroll
-    for (int k = 0; k < SL_MAX_EXITS; k++) {
-        w.tgt[k] = -1;
-        w.val[k] = 0;
-        if (k < w.ne) {
-            const int iy = st.exit_y[b * SL_MAX_EXITS + k], ix = st.exit_x[b * SL_MAX_EXITS + k];
-            int jy = pymod(iy - y0 + H / 2, H) - H / 2;
-            int jx = pymod(ix - x0 + W / 2, W) - W / 2;
-            jy = min(max(jy + a.vh / 2, 0), a.vh - 1);
-            jx = min(max(jx + a.vw / 2, 0), a.vw - 1);
-            w.tgt[k] = jy * a.vw + jx;
-            w.val[k] = obs_value(w.gb[iy * W + ix], w.gg[iy * W + ix], a.remove_white);
-        }
-    }
-}
-
-// values of the cells i = i0 + 64g (g < kObsGroup); (r, c) = position of i0, advanced
-template <class F>
-__device__ __forceinline__ void obs_wave_cells(const sl_env_state &st, const ObsArgs &a,
-                                               const ObsWave &w, int nv, int &i0, int &r, int &c,
-                                               F &&emit) {
-    const int dr = 64 / a.vw, dc = 64 - dr * a.vw;
-    uint32_t bv[kObsGroup], gv[kObsGroup];
-#pragma unroll
-    for (int g = 0; g < kObsGroup; g++) {
-        bv[g] = 0;
-        gv[g] = 0;
-        if (i0 + 64 * g < nv) {
-            const int src = pymod(w.ty + r, st.H) * st.W + pymod(w.tx + c, st.W);
-            bv[g] = w.gb[src];
-            gv[g] = w.gg[src];
-        }
-        r += dr;
-        c += dc;
-        if (c >= a.vw) {
-            c -= a.vw;
-            r++;
-        }
-    }
-#pragma unroll
-    for (int g = 0; g < kObsGroup; g++) {
-        const int i = i0 + 64 * g;
-        if (i < nv) {
-            uint32_t v = obs_value(bv[g], gv[g], a.remove_white);
-#pragma unroll
-            for (int k = 0; k < SL_MAX_EXITS; k++)
-                if (k < w.ne && i == w.tgt[k]) v = w.val[k];
-            emit(i, v);
-        }
-    }
-    i0 += 64 * kObsGroup;
-}
-
-__device__ __forceinline__ void obs_packed_wave(const sl_env_state &st, const ObsArgs &a,
-                                                int64_t b, int lane, uint16_t *__restrict__ out) {
-    ObsWave w;
-    obs_wave_init(st, a, b, w);
-    const int nv = a.vh * a.vw;
-    uint16_t *o = out + b * nv;
-    int i0 = lane, r = lane / a.vw, c = lane - (lane / a.vw) * a.vw;
-    while (i0 < nv)
-        obs_wave_cells(st, a, w, nv, i0, r, c, [&](int i, uint32_t v) { o[i] = (uint16_t)v; });
-}
-
 __global__ void __launch_bounds__(256)
 k_env_obs_packed(sl_env_state st, ObsArgs a, uint16_t *__restrict__ out) {
     const int64_t b = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (b >= st.B) return;
     obs_packed_wave(st, a, b, threadIdx.x & 63, out);
-}
-
-// packed obs of the envs the 64x64 step kernel queued for reset, after
-// k_env_reset_list reset them (the step kernel wrote every other env's view)
-__global__ void __launch_bounds__(256)
-k_env_obs_packed_list(sl_env_state st, ObsArgs a, uint16_t *__restrict__ out,
-                      const int64_t *__restrict__ scratch, uint32_t step) {
-    const int n = (int)__builtin_amdgcn_readfirstlane((int)scratch[8 * st.B + 2 + (step & 1)]);
-    const int32_t *list = reinterpret_cast<const int32_t *>(scratch + 2 * st.B);
-    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    for (int i = blockIdx.x * 4 + wid; i < n; i += gridDim.x * 4)
-        obs_packed_wave(st, a, __builtin_amdgcn_readfirstlane(list[i]), threadIdx.x & 63, out);
 }
 
 // channel obs.  Per view cell the wave first stores in LDS the cell's CHANNEL MASK
@@ -922,17 +810,6 @@ int launch_obs(const sl_env_state &st, const ObsArgs &a, void *out, hipStream_t 
 }  // namespace
 
 namespace sl {
-int launch_obs_packed_list(const sl_env_state &st, int vh, int vw, int remove_white,
-                           uint16_t *out, const int64_t *scratch, uint32_t step, hipStream_t s) {
-    ObsArgs a;
-    int rc = obs_args(vh, vw, remove_white, SL_OBS_PACKED, nullptr, 0, &a);
-    if (rc) return rc;
-    const unsigned grid = (unsigned)(st.B < 1024 ? (st.B + 3) / 4 : 256);
-    hipLaunchKernelGGL(k_env_obs_packed_list, dim3(grid), dim3(256), 0, s, st, a, out, scratch,
-                       step);
-    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
-}
-
 int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
                            int64_t *scratch, uint32_t step, hipStream_t s) {
     const unsigned grid = (unsigned)(st.B < 256 ? st.B : 256);
@@ -1106,9 +983,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     if (cfg->obs_out) {
         if (!fuse_obs || (cfg->auto_reset && !reset_done))
             return launch_obs(*st, oa, cfg->obs_out, s);
-        if (reset_done)      // views of the envs reset after the step kernel wrote theirs
-            return launch_obs_packed_list(*st, oa.vh, oa.vw, oa.remove_white,
-                                          (uint16_t *)cfg->obs_out, cfg->scratch, cfg->step, s);
+        // else: the reset-list kernel wrote the views of the envs it reset
     }
     return SL_OK;
 }

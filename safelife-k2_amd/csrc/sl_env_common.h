@@ -244,10 +244,6 @@ struct FastExtra {
     uint16_t *obs_out;      // 64x64 kernel: packed views written from the on-chip
     int32_t obs_vh, obs_vw, obs_rw;   // board (NULL: none); view shape, remove_white
 };
-// packed views of the envs queued for reset in the scratch list of step `step`
-// (after their reset), one wave each (sl_env.hip)
-int launch_obs_packed_list(const sl_env_state &st, int vh, int vw, int remove_white,
-                           uint16_t *out, const int64_t *scratch, uint32_t step, hipStream_t s);
 bool fast_shape(int H, int W);
 int launch_step_fast(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
