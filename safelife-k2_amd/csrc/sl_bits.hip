@@ -759,6 +759,7 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         hipLaunchKernelGGL(k_env_step_bits64<false>, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, ka);
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
+    if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);
     if (fx.fuse_reset && fx.pool.K > 0) {
         const unsigned grid = (unsigned)(st.B < 512 ? st.B : 512);
         sl::obs::ObsArgs oa{};

@@ -496,6 +496,7 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
     const Step128KArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
     hipLaunchKernelGGL(k_env_step_bits128, dim3((unsigned)st.B), dim3(64), 0, s, ka);
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
+    if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);
     if (fx.fuse_reset && fx.pool.K > 0)
         return launch_reset_list_wide(st, fx.pool, fx.ra, fx.scratch, a.step, s);
     return SL_OK;

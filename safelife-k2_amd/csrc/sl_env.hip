@@ -912,6 +912,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     else fx.pool = sl_level_pool{};
     fx.ra = reset_args(cfg);
     fx.scratch = cfg->scratch;
+    fx.ev_end = cfg->ev_end;
     // observations: packed views of 64x64 boards come out of the step kernel itself
     ObsArgs oa;
     if (cfg->obs_out) {
@@ -973,7 +974,9 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         }
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
-    if (cfg->ev_end) (void)hipEventRecord((hipEvent_t)cfg->ev_end, s);
+    // the bit-sliced 64x64 / 128x128 launchers record ev_end themselves, between the
+    // step kernel and their reset-list kernel
+    if (cfg->ev_end && !fast && !fast128) (void)hipEventRecord((hipEvent_t)cfg->ev_end, s);
 
     if (cfg->auto_reset && !reset_done) {
         hipLaunchKernelGGL(k_env_reset_scan, dim3((unsigned)((B + NT - 1) / NT)), dim3(NT), 0, s,

@@ -241,6 +241,8 @@ struct FastExtra {
     int32_t fuse_reset;     // auto-reset: the step kernel lists finished envs and a
                             // follow-up kernel resets exactly those
     int64_t *scratch;       // sl_env_cfg.scratch (reset list + counters)
+    void *ev_end;           // hipEvent_t recorded right after the step kernel's launch
+                            // (before any follow-up kernel), or NULL
     uint16_t *obs_out;      // 64x64 kernel: packed views written from the on-chip
     int32_t obs_vh, obs_vw, obs_rw;   // board (NULL: none); view shape, remove_white
 };

@@ -596,11 +596,11 @@ int launch_step_fast(const sl_env_state &st, const StepArgs &a, const FastExtra 
     hipLaunchKernelGGL((k_env_step_w64_lds<64, SL_FAST_UNR>), dim3((unsigned)st.B), dim3(128), 0,
                        s, st, a, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
 #else
-    (void)fx;
     const unsigned grid = (unsigned)((st.B + 3) / 4);
     hipLaunchKernelGGL((k_env_step_w64<64, SL_FAST_UNR>), dim3(grid), dim3(256), 0, s, st, a,
                        actions, ctp, ctc, reward, done, flags, ep_len, ep_rew);
 #endif
+    if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
