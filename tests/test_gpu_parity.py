@@ -547,6 +547,46 @@ def test_bitsliced_kernels_tiny_batches(torch_dev, B):
             _compare_state(fast, gen, ctx)
 
 
+def test_c_abi_rejects_bad_arguments(torch_dev):
+    """The C ABI returns SL_EINVAL (no launch) for bad view shapes, observation modes,
+    channel lists and movement-bonus periods, and SL_ETOOBIG when a bit-sliced kernel
+    is required for a shape none takes."""
+    import ctypes
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool, _lib
+    L = _lib.lib()
+    pool = LevelPool.load(os.path.join(GOLDEN, "pools", "c3_prune_still_64.npz"))
+    env = SafeLifeVecEnv(pool, 4, "cuda:0", output_channels=None, view_shape=(15, 15))
+    env.reset()
+    st, sp = ctypes.byref(env._state), _lib.stream_ptr(dev)
+    out = torch.zeros(4 * 70 * 70 * 16, dtype=torch.int32, device=dev)
+    chans = (ctypes.c_int32 * 2)(0, 16)
+    assert L.sl_env_obs(st, 0, 5, 1, _lib.SL_OBS_PACKED, None, 0, out.data_ptr(), sp) == _lib.SL_EINVAL
+    assert L.sl_env_obs(st, 5, 5, 1, 99, None, 0, out.data_ptr(), sp) == _lib.SL_EINVAL
+    assert L.sl_env_obs(st, 5, 5, 1, _lib.SL_OBS_CHANNELS, chans, 2, out.data_ptr(), sp) == _lib.SL_EINVAL
+    assert L.sl_env_obs(st, 5, 5, 1, _lib.SL_OBS_CHANNELS, None, 0, out.data_ptr(), sp) == _lib.SL_EINVAL
+    a = torch.zeros(4, dtype=torch.int32, device=dev)
+    cfg = env._fill_cfg()
+    env._fill_obs_cfg(cfg, None)
+    args = (st, ctypes.byref(env._pool_dev["struct"]), a.data_ptr(), ctypes.byref(cfg),
+            env.reward.data_ptr(), env.done.data_ptr(), env.flags.data_ptr(),
+            env.ep_len.data_ptr(), env.ep_rew.data_ptr(), sp)
+    cfg.bonus_period = 17
+    assert L.sl_env_step(*args) == _lib.SL_EINVAL
+    cfg.bonus_period = env.movement_bonus_period
+    cfg.obs_out = out.data_ptr()
+    cfg.obs_mode, cfg.obs_vh, cfg.obs_vw = _lib.SL_OBS_PACKED, 0, 15     # empty view
+    assert L.sl_env_step(*args) == _lib.SL_EINVAL
+    cfg.obs_mode, cfg.obs_vh = 42, 15                                      # no such mode
+    assert L.sl_env_step(*args) == _lib.SL_EINVAL
+    torch.cuda.synchronize()
+    odd = LevelPool(np.zeros((1, 40, 70), np.uint16), np.zeros((1, 40, 70), np.uint16),
+                    [(0, 0)], [1], [0.3], [0.01])
+    with pytest.raises(RuntimeError):
+        SafeLifeVecEnv(odd, 2, "cuda:0", kernel="fast", output_channels=None).step(
+            torch.zeros(2, dtype=torch.int32, device=dev))
+
+
 # ------------------------------------------------ 128x128 bit-sliced kernel (C5)
 C5_POOL = os.path.join(GOLDEN, "pools", "c5_navigation_128.npz")
 
