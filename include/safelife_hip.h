@@ -73,6 +73,7 @@ extern "C" {
 
 /* Library / device info. */
 const char *sl_version(void);
+const char *sl_build_id(void);   /* hash of the sources this library was built from */
 int sl_device_arch(char *buf, int len);   /* e.g. "gfx950" */
 
 /* Timing events (hipEvent_t as void*) for in-process kernel timing. */
@@ -240,7 +241,15 @@ typedef struct sl_env_cfg {
     const double *draws;            /* SL_RNG_STREAM: dev uniform stream       */
     int64_t n_draws;
     int64_t *stream_pos;            /* dev [1]: next unread draw (advanced)    */
-    int64_t *scratch;               /* dev [8*B + 16] workspace               */
+    int64_t *scratch;               /* dev [8*B + 16] workspace, zeroed once
+                                     * before the first step.  With auto_reset the
+                                     * 64x64 / 128x128 kernels queue finished envs
+                                     * in per-parity lists (words 8B+2, 8B+3) that
+                                     * stay valid only over consecutive steps
+                                     * (step, step+1, ...) with auto_reset set: zero
+                                     * words 8B+2..8B+3 again after any other
+                                     * sequence (rewound step index, auto_reset
+                                     * toggled, state written by the caller)     */
     int32_t level_mode;             /* 0: level = (env0+b + episodes*n_total)%K,
                                        1: Philox-random level                  */
     int32_t n_total_envs;           /* envs across all shards                  */

@@ -64,6 +64,15 @@ def lib():
         L.orc_count_eligible.argtypes = [vp, ctypes.c_int, ctypes.c_int]
         L.orc_philox_uniform.restype = ctypes.c_double
         L.orc_philox_uniform.argtypes = [u32, u32, u32, u32, u64]
+        L.orc_batch_create.restype = vp
+        L.orc_batch_create.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64]
+        L.orc_batch_free.argtypes = [vp]
+        L.orc_batch_reset.argtypes = [vp, vp, vp]
+        L.orc_batch_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
+        L.orc_batch_board.restype = ctypes.POINTER(ctypes.c_uint16)
+        L.orc_batch_board.argtypes = [vp, i64, ctypes.c_int]
+        L.orc_batch_scalars.argtypes = [vp, i64, vp]
+        L.orc_max_threads.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -317,6 +326,30 @@ class Level:
                      self.spawn_prob, self.min_performance)
 
 
+def pool_level_fn(levels, gid, seed=0, n_total=1, random_order=False, augment=False):
+    """The level (and toroidal roll) of global env ``gid``'s episode ``ep`` as the
+    device level pool hands it out (sl_env_common.h choose_level): in pool order
+    (gid + ep * n_total) mod K, or Philox-random; rolled by Philox offsets when
+    ``augment``.  This replaces the reference's level iterator
+    (file_finder.py:143-201) with a deterministic per-env choice, so the oracle must
+    make the same choice to follow an env across resets."""
+    K = len(levels)
+
+    def fn(ep):
+        if random_order:
+            idx = int(philox_uniform(gid, ep, 0x5EED, 2, seed) * K)
+        else:
+            idx = (gid + ep * n_total) % K
+        lv = levels[min(max(idx, 0), K - 1)]
+        if augment:
+            H, W = lv.board.shape
+            dy = min(int(philox_uniform(gid, ep, 0x0011, 3, seed) * H), H - 1)
+            dx = min(int(philox_uniform(gid, ep, 0x0022, 3, seed) * W), W - 1)
+            lv = lv.rolled(dy, dx)
+        return lv
+    return fn
+
+
 class OracleEnv:
     """Per-env restatement of the PPO wrapper chain (see module docstring)."""
 
@@ -341,7 +374,8 @@ class OracleEnv:
         self.step_counter = 0               # global batched-step index (philox)
         self.can_toggle_powers = can_toggle_powers
         self.can_toggle_colors = can_toggle_colors
-        self.episodes = 0
+        self.episodes = 0                   # global_counter.episodes_started (this env)
+        self.completed = 0                  # global_counter.episodes_completed
 
     # ---- game-level pieces -------------------------------------------------
     def _relative_loc(self, n_forward, n_right=0):
@@ -480,7 +514,10 @@ class OracleEnv:
         self.episode_reward += reward
         self._update_exit_colors()
         times_up = self.episode_length > self.time_limit
+        already_completed = self.episode_completed
         self.episode_completed = times_up or self.game_over
+        if not already_completed:           # safelife_env.py:169-175
+            self.completed += int(self.episode_completed)
         info = {"times_up": times_up, "episode_length": self.episode_length,
                 "episode_reward": int(self.episode_reward),
                 "game_over": bool(self.game_over)}
@@ -515,6 +552,142 @@ class OracleEnv:
             obs = self.reset()
         self.step_counter += 1
         return obs, float(reward), done, info
+
+
+    def load_state(self, s, step_counter):
+        """Continue from a mid-episode state taken from a batched env: ``s`` maps the
+        per-env fields of SafeLifeVecEnv (board, goals, start_board, agent_x, ...,
+        prior ring, exits) to this env's values; ``step_counter`` is the batched
+        step index of the next step (the Philox counter)."""
+        self.board = np.array(s["board"], dtype=np.uint16)
+        self.goals = np.array(s["goals"], dtype=np.uint16)
+        self.init_board = np.array(s["start_board"], dtype=np.uint16)
+        self.init_goals = None              # only the reset reads it (baseline below)
+        self.agent_loc = (int(s["agent_x"]), int(s["agent_y"]))
+        self.orientation = int(s["orientation"])
+        self.game_over = bool(s["game_over"])
+        self.num_steps = int(s["num_steps"])
+        self.episode_length = int(s["episode_length"])
+        self.episode_reward = int(s["episode_reward"])
+        self.episode_completed = bool(self.game_over or
+                                      self.episode_length > self.time_limit)
+        self.old_points = int(s["old_points"])
+        self.baseline = int(s["baseline"])
+        self.spawn_prob = float(s["spawn_prob"])
+        self.min_performance = float(s["min_performance"])
+        self.last_side_effect = int(s["side_effect"])
+        n = int(s["exit_count"])
+        self.exits = [(int(s["exit_y"][k]), int(s["exit_x"][k])) for k in range(n)]
+        self.exit_mask = (self.init_board & EXIT) > 0
+        period = self.mb[2]
+        ln, hd = int(s["prior_len"]), int(s["prior_head"])
+        self.prior = [(int(s["prior_x"][(hd + k) % period]), int(s["prior_y"][(hd + k) % period]))
+                      for k in range(ln)]
+        self.episodes = int(s["episodes"])
+        self.step_counter = int(step_counter)
+
+
+# ---------------------------------------------------------------------------
+# The same chain compiled (sl_cpu_step.c): bench.py's CPU baseline
+# ---------------------------------------------------------------------------
+class _Pool(ctypes.Structure):
+    _fields_ = [("K", ctypes.c_int32), ("H", ctypes.c_int32), ("W", ctypes.c_int32),
+                ("board", ctypes.c_void_p), ("goals", ctypes.c_void_p),
+                ("agent_x", ctypes.c_void_p), ("agent_y", ctypes.c_void_p),
+                ("orientation", ctypes.c_void_p), ("spawn_prob", ctypes.c_void_p),
+                ("min_performance", ctypes.c_void_p)]
+
+
+class _Cfg(ctypes.Structure):
+    _fields_ = [("time_limit", ctypes.c_int32), ("view_h", ctypes.c_int32),
+                ("view_w", ctypes.c_int32), ("remove_white", ctypes.c_int32),
+                ("obs", ctypes.c_int32), ("bonus_period", ctypes.c_int32),
+                ("level_random", ctypes.c_int32), ("augment", ctypes.c_int32),
+                ("n_total", ctypes.c_int32), ("penalty_coef", ctypes.c_double),
+                ("wrapper_min_perf", ctypes.c_double), ("bonus", ctypes.c_double),
+                ("bonus_power", ctypes.c_double), ("seed", ctypes.c_uint64)]
+
+
+class CpuBatch:
+    """B envs of the PPO chain stepped by sl_cpu_step.c (Philox spawns; levels from a
+    pool as pool_level_fn picks them).  Same results as B OracleEnv's."""
+
+    SCALARS = ("agent_x", "agent_y", "orientation", "game_over", "episode_length",
+               "episode_reward", "old_points", "baseline", "side_effect", "episodes",
+               "completed", "exit_count")
+
+    def __init__(self, levels, num_envs, env0=0, time_limit=1000, view_shape=(15, 15),
+                 remove_white_goals=True, movement_bonus=0.1, movement_bonus_power=0.01,
+                 movement_bonus_period=4, penalty_coef=0.0, min_performance=0.01, seed=0,
+                 level_order="sequential", augment_roll=False, n_total_envs=None, obs=False):
+        L = lib()
+        self.B = int(num_envs)
+        self.H, self.W = levels[0].board.shape
+        self._arr = dict(
+            board=np.ascontiguousarray(np.stack([lv.board for lv in levels]), np.uint16),
+            goals=np.ascontiguousarray(np.stack([lv.goals for lv in levels]), np.uint16),
+            agent_x=np.array([lv.agent_loc[0] for lv in levels], np.int32),
+            agent_y=np.array([lv.agent_loc[1] for lv in levels], np.int32),
+            orientation=np.array([lv.orientation for lv in levels], np.int32),
+            spawn_prob=np.array([lv.spawn_prob for lv in levels], np.float64),
+            min_performance=np.array([lv.min_performance for lv in levels], np.float64))
+        p = _Pool()
+        p.K, p.H, p.W = len(levels), self.H, self.W
+        for k, v in self._arr.items():
+            setattr(p, k, v.ctypes.data)
+        self._pool = p
+        c = _Cfg()
+        c.time_limit = int(time_limit)
+        c.view_h, c.view_w = (int(v) for v in view_shape)
+        c.remove_white = int(bool(remove_white_goals))
+        c.obs = int(bool(obs))
+        c.bonus_period = int(movement_bonus_period)
+        c.level_random = int(level_order == "random")
+        c.augment = int(bool(augment_roll))
+        c.n_total = int(n_total_envs or self.B)
+        c.penalty_coef = float(penalty_coef)
+        c.wrapper_min_perf = float(min_performance)
+        c.bonus = float(movement_bonus)
+        c.bonus_power = float(movement_bonus_power)
+        c.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self._cfg = c
+        self._h = L.orc_batch_create(self.B, self.H, self.W, int(env0))
+        if not self._h:
+            raise MemoryError("orc_batch_create")
+        self.reward = np.zeros(self.B, np.float64)
+        self.done = np.zeros(self.B, np.uint8)
+        self.obs = np.zeros((self.B,) + tuple(view_shape), np.uint16) if obs else None
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and _lib is not None:
+            _lib.orc_batch_free(h)
+
+    def reset(self):
+        if lib().orc_batch_reset(self._h, ctypes.byref(self._pool), ctypes.byref(self._cfg)):
+            raise ValueError("orc_batch_reset: bad pool or config")
+
+    def step(self, actions, threads=0):
+        a = np.ascontiguousarray(actions, dtype=np.int32)
+        assert a.shape == (self.B,)
+        lib().orc_batch_step(self._h, a.ctypes.data, ctypes.byref(self._pool),
+                             ctypes.byref(self._cfg), self.reward.ctypes.data,
+                             self.done.ctypes.data,
+                             self.obs.ctypes.data if self.obs is not None else None, int(threads))
+        return self.obs, self.reward, self.done
+
+    def board(self, i, which=0):
+        ptr = lib().orc_batch_board(self._h, int(i), int(which))
+        return np.ctypeslib.as_array(ptr, shape=(self.H, self.W)).copy()
+
+    def scalars(self, i):
+        out = np.zeros(12, np.int64)
+        lib().orc_batch_scalars(self._h, int(i), out.ctypes.data)
+        return dict(zip(self.SCALARS, out.tolist()))
+
+
+def max_threads():
+    return int(lib().orc_max_threads())
 
 
 # ---------------------------------------------------------------------------

@@ -1,5 +1,5 @@
-// sl_action.h -- pieces shared by the fused 64-wide step kernels (sl_fast.hip,
-// sl_bits.hip): the score lookup table and the single-lane action evaluator.
+// sl_action.h -- pieces shared by the fused bit-sliced step kernels (sl_bits.hip,
+// sl_bits128.hip, sl_bits_small.hip): the score lookup table and the single-lane action evaluator.
 #pragma once
 #include "sl_env_common.h"
 

@@ -12,14 +12,10 @@
 //   g.horiz(w0, w1)  columns col0-1 / col0+2 of a per-word quantity;
 //   g.halo_spawn()   a spawner sits in a row just outside the wave's words;
 //   g.cell(y, w)     the cell's flat index (the Philox counter of its draw);
-//   g.draws(...)     the spawn draws of the eligible cells (lane_draws or wave_draws).
+//   g.draws(...)     the spawn draws of the eligible cells (lane_draws).
 #pragma once
 #include "sl_action.h"
 
-// timing-only ablation (results are wrong when set; never in the shipped build)
-#ifndef SL_RULE_NO_DRAWS
-#define SL_RULE_NO_DRAWS 0
-#endif
 
 namespace sl {
 namespace bits {
@@ -152,55 +148,6 @@ __device__ __forceinline__ void lane_draws(const Geo &g, const u32 elig[2], u32 
     }
 }
 
-// The same draws shared out over the wave: every lane appends its eligible cells to
-// a list in LDS (an LDS atomic hands out the slots), the wave draws the list 64
-// entries at a time, and each hit is OR-ed into its owner's result word.  A wave
-// then takes ceil(n / 64) Philox evaluations for n eligible cells.  Entries are
-// (lane << 6) | (w << 5) | y; g.cell_at(lane, y, w) gives the cell's flat index.
-// LDS: list[64 * 64] u16, res[128] u32, cnt[1] u32, private to the wave.
-typedef __attribute__((address_space(3))) uint16_t lds_u16_t;
-typedef __attribute__((address_space(3))) u32 lds_u32_t;
-struct DrawLds {
-    lds_u16_t *list;
-    lds_u32_t *res;
-    lds_u32_t *cnt;
-};
-template <class Geo>
-__device__ __forceinline__ void wave_draws(const Geo &g, const u32 elig[2], u32 sp[2],
-                                           const SpawnCtx &sc, u32 tensor, const DrawLds &d,
-                                           int lane) {
-    d.res[2 * lane] = 0u;
-    d.res[2 * lane + 1] = 0u;
-    if (lane == 0) *d.cnt = 0u;
-    wait_lgkm();
-    const u32 n = (u32)(__builtin_popcount(elig[0]) + __builtin_popcount(elig[1]));
-    u32 o = __hip_atomic_fetch_add(d.cnt, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#pragma unroll
-    for (int w = 0; w < 2; w++) {
-        u32 e = elig[w];
-        while (e) {
-            const int y = __builtin_ctz(e);
-            e &= e - 1;
-            d.list[o++] = (uint16_t)((lane << 6) | (w << 5) | y);
-        }
-    }
-    wait_lgkm();
-    const int total = (int)__builtin_amdgcn_readfirstlane((int)*d.cnt);
-    for (int base = 0; base < total; base += 64) {
-        const int i = base + lane;
-        if (i < total) {
-            const u32 ent = d.list[i];
-            const int l = (int)(ent >> 6), w = (int)((ent >> 5) & 1u), y = (int)(ent & 31u);
-            if (philox_uniform(g.cell_at(l, y, w), sc.gid, sc.step, tensor, sc.seed) < sc.thr)
-                __hip_atomic_fetch_or(d.res + 2 * l + w, 1u << y, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WAVEFRONT);
-        }
-    }
-    wait_lgkm();
-    sp[0] = d.res[2 * lane];
-    sp[1] = d.res[2 * lane + 1];
-}
-
 // One CA step of the planes P (in place).  chg[w] = cells that changed.
 // Appendix A: alive x survives iff frozen | P | cnt in {3,4}; dead x unless frozen | I
 // is born iff cnt == 3 (colours: >= 2 alive of a colour, or any spawner of it;
@@ -304,7 +251,7 @@ __device__ __forceinline__ void rule_planes(u32 P[32], u32 chg[2], const Geo &g,
             colk[k][0] |= h.l0 | vsc[k][0] | vsc[k][1];
             colk[k][1] |= vsc[k][0] | vsc[k][1] | h.r1;
         }
-        if (SL_RULE_NO_DRAWS || sc.thr <= 0.0) {            // u < p never holds
+        if (sc.thr <= 0.0) {            // u < p never holds
         } else if (sc.thr >= 1.0) {                         // u < p always holds
             sp[0] = elig[0];
             sp[1] = elig[1];

@@ -1,8 +1,7 @@
 // sl_bits.hip -- the bit-sliced fused env-step kernel for 64x64 boards.
 //
-// Same semantics as k_env_action + k_env_step_generic (sl_env.hip) and the
-// packed fast kernel (sl_fast.hip); different data layout, chosen for CDNA4's
-// VALU-issue limit:
+// Same semantics as k_env_action + k_env_step_generic (sl_env.hip); different data
+// layout, chosen for CDNA4's VALU-issue limit:
 //
 //  * one wave64 per env; lane l owns the column pair (2j, 2j+1), j = l >> 1, for
 //    the 32-row half h = l & 1 (rows 32h .. 32h+31);
@@ -39,37 +38,8 @@ using namespace sl::bits;
 
 namespace {
 
-#ifndef SL_BITS_WPB
-#define SL_BITS_WPB 1        // envs (waves) per workgroup
-#endif
-#ifndef SL_BITS_UACT
-#define SL_BITS_UACT 0       // 1: the action runs wave-uniform (scalar unit); 0: on lane 0
-#endif
-#ifndef SL_BITS_UEPI
-#define SL_BITS_UEPI 0       // 1: the epilogue runs wave-uniform; 0: on lane 0
-#endif
-// timing-only ablations (results are wrong when set; never in the shipped build):
-//   1 no goals rule, 2 no board rule, 4 no scoring, 8 no board row stores,
-//   16 no action / epilogue
-#ifndef SL_BITS_ABL
-#define SL_BITS_ABL 0
-#endif
-#ifndef SL_BITS_MIRROR
-#define SL_BITS_MIRROR 1     // keep / use the bit-plane mirror of the goals
-#endif
-#ifndef SL_BITS_MINW
-#define SL_BITS_MINW 4       // waves per SIMD the register budget is sized for
-#endif
-#ifndef SL_BITS_PERSIST
-#define SL_BITS_PERSIST 0    // persistent waves: the next env's board, record and goal
-                             // colour planes are loaded while this env finishes
-#endif
-#ifndef SL_BITS_WAVES_PER_CU
-#define SL_BITS_WAVES_PER_CU 16   // persistent grid: waves per CU
-#endif
-#ifndef SL_BITS_MINW_OBS
-#define SL_BITS_MINW_OBS 3   // the same for the instantiation that writes observations
-#endif
+constexpr int kMinWaves = 4;      // waves per SIMD the register budget is sized for
+constexpr int kMinWavesObs = 3;   // the same for the instantiation that writes views
 
 constexpr int N = 64;        // rows = columns = lanes
 
@@ -222,7 +192,7 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
 #pragma unroll
     for (int y = 0; y < 32; y++) gg[y * 32] = P[y];
     transpose32(P);
-    u32 *mg = (SL_BITS_MIRROR && st.planes) ? st.planes + b * 4096 + 2048 + lane : nullptr;
+    u32 *mg = st.planes ? st.planes + b * 4096 + 2048 + lane : nullptr;
     if (mg) {      // the goals' bit-plane mirror
 #pragma unroll
         for (int q = 0; q < 32; q++) mg[q * 64] = P[q];
@@ -299,7 +269,7 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
 }
 
 // all kernel arguments of k_env_step_bits64 in one struct at kernarg offset 0, so a
-// phase can re-read one late through kernarg() (see the persistent loop, write_obs)
+// phase can re-read one late through kernarg() (write_obs)
 struct StepKArgs {
     sl_env_state st;
     StepArgs a;
@@ -420,7 +390,7 @@ struct Pre {
 __device__ __forceinline__ void issue_pre(const sl_env_state &st, const int32_t *actions,
                                           int64_t b, int lane, Pre &p) {
     p.V = load_record(st, actions, b, lane);
-    if (SL_BITS_MIRROR && st.planes) {
+    if (st.planes) {
         const u32 *mg = st.planes + b * 4096 + 2048 + lane;
 #pragma unroll
         for (int k = 0; k < 3; k++) {
@@ -431,15 +401,14 @@ __device__ __forceinline__ void issue_pre(const sl_env_state &st, const int32_t 
 }
 
 // One env-step of env b.  `pre` holds b's record and goal colour planes and b's board
-// is in flight into `buf` (issued by the caller).  With PF, the same is issued for
-// env bn (< 0: none) as soon as this env no longer needs the buffer / registers.
-template <bool OBS, bool PF>
+// is in flight into `buf` (issued by the caller).
+template <bool OBS>
 __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs &a,
                                          const FastExtra &fx, int64_t b, int lane, lds_u32 *buf,
                                          const int32_t *__restrict__ actions, int ctp, int ctc,
                                          double *reward_out, uint8_t *done_out,
                                          uint8_t *flags_out, int32_t *ep_len_out,
-                                         int32_t *ep_rew_out, Pre &pre, int64_t bn) {
+                                         int32_t *ep_rew_out, const Pre &pre) {
     const int64_t off = b * (int64_t)(N * N);
     const int lane_off = (lane & 1) * 1024 + (lane >> 1);     // dwords: row 32h, column pair j
     u32 *gb = reinterpret_cast<u32 *>(st.board + off) + lane_off;
@@ -448,7 +417,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     // goals mirror, word-major: word q of lane l at planes[b*4096 + 2048 + q*64 + l]
     // (the goals rarely change, so it saves their transpose at almost no write cost;
     // a board mirror would be rewritten every step and does not pay)
-    u32 *mg = (SL_BITS_MIRROR && st.planes) ? st.planes + b * 4096 + 2048 + lane : nullptr;
+    u32 *mg = st.planes ? st.planes + b * 4096 + 2048 + lane : nullptr;
     const u32 V = pre.V;
     // goals: a goals board without spawners that came through a step unchanged is at
     // a fixed point of the (then deterministic) rule and never changes again
@@ -479,8 +448,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
             transpose32(PG);
         }
         u32 cg[2];
-        if (SL_BITS_ABL & 1) { cg[0] = cg[1] = 0; asm volatile("" : "+v"(PG[0])); }
-        else rule_planes(PG, cg, Geo64{lane}, sc, 1u);
+        rule_planes(PG, cg, Geo64{lane}, sc, 1u);
         const u32 rg = wave_or(cg[0] | cg[1]);
         if (mg) {      // mirror: the words whose 32 cells changed (all of them if rebuilt)
             const bool all = !(pok & 2);
@@ -523,7 +491,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
                rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     int act_reward = 0;
-    if (!(SL_BITS_ABL & 16) && (SL_BITS_UACT || lane == 0))
+    if (lane == 0)
         act_reward = act_core(env, rec(V, R_ACT), N, N, ctp, ctc, ov);
     act_reward = __builtin_amdgcn_readfirstlane(act_reward);
     const int ne = __builtin_amdgcn_readfirstlane(ov.n);
@@ -566,8 +534,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         }
     }
     u32 cb[2];
-    if (SL_BITS_ABL & 2) { cb[0] = PB[0] & 1; cb[1] = 0; }
-    else rule_planes(PB, cb, Geo64{lane}, sc, 0u);
+    rule_planes(PB, cb, Geo64{lane}, sc, 0u);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- scores over the new board and goals
@@ -580,16 +547,11 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         transpose32(PS);
     }
     int pts, scr, pos, side;
-    if (SL_BITS_ABL & 4) { pts = PB[3] & 3; scr = PS[5] & 1; pos = gcol[0][1] & 1; side = 0; }
-    else score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
+    score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
     // totals (packed two per word: per-lane ranges [-192, 320] and [-64, 64]);
     // reduced before the board store so the scoring is not sunk past it
     const int s1 = wave_total((pts + 192) | ((scr + 64) << 16));
     const int s2 = wave_total(pos | (side << 16));
-    if (PF && !OBS && bn >= 0) {        // the buffer has been read out: next env's board
-        wait_lgkm();
-        dma_board(st.board + bn * (int64_t)(N * N), buf, lane);
-    }
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- write back the changed rows of the board, exits already in the colour the
@@ -600,7 +562,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     const int possible = s2 & 0xFFFF;
     const int side_total = (s2 >> 16) & 0xFFFF;
     const u32 rb = wave_or(cb[0] | cb[1]) | erow;
-    if ((rb || OBS) && !(SL_BITS_ABL & 8)) {
+    if (rb || OBS) {
         const bool can = can_exit_now(fl.min_performance(), score, fl.baseline(), possible);
 #pragma unroll
         for (int w = 0; w < 2; w++)
@@ -646,20 +608,13 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
             }
         }
     }
-    if (OBS && !(SL_BITS_ABL & 8)) {
+    if (OBS) {
         __builtin_amdgcn_sched_barrier(0);
         write_obs(buf, fx, fl, b, lane);
         __builtin_amdgcn_sched_barrier(0);
     }
-    if (PF && bn >= 0) {
-        if (OBS) {
-            wait_lgkm();
-            dma_board(st.board + bn * (int64_t)(N * N), buf, lane);
-        }
-        issue_pre(st, actions, bn, lane, pre);
-    }
     int reset = 0;
-    if (!(SL_BITS_ABL & 16) && (SL_BITS_UEPI || lane == 0))
+    if (lane == 0)
         reset = epilogue_core(st, a, b, fl, act_reward, points, score, possible, side_total,
                               reward_out, done_out, flags_out, ep_len_out, ep_rew_out);
     reset = __builtin_amdgcn_readfirstlane(reset);
@@ -673,38 +628,17 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
 
 // OBS: also write the packed observation (fx.obs_out)
 template <bool OBS>
-__global__ void __launch_bounds__(64 * SL_BITS_WPB, OBS ? SL_BITS_MINW_OBS : SL_BITS_MINW)
+__global__ void __launch_bounds__(64, OBS ? kMinWavesObs : kMinWaves)
 k_env_step_bits64(StepKArgs ka) {
-    const int64_t b = (int64_t)blockIdx.x * SL_BITS_WPB +
-                      __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = threadIdx.x & 63;
-    __shared__ __attribute__((aligned(16))) u32 stage[SL_BITS_WPB][N * N / 2];
-    if (b >= ka.st.B) return;              // whole waves only
-    lds_u32 *buf = (lds_u32 *)&stage[threadIdx.x >> 6][0];
+    const int64_t b = blockIdx.x;          // one wave per env
+    const int lane = threadIdx.x;
+    __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
+    lds_u32 *buf = (lds_u32 *)&stage[0];
     Pre pre;
     issue_pre(ka.st, ka.actions, b, lane, pre);
     dma_board(ka.st.board + b * (int64_t)(N * N), buf, lane);
-    if (SL_BITS_PERSIST) {
-        // persistent waves, static stride over the envs; every wave leaves the loop
-        // after at most ceil(B / waves) iterations.  The arguments are re-read from
-        // the kernarg segment in every iteration through a pointer the compiler cannot
-        // see as loop-invariant: hoisted, the ~60 argument dwords would not fit in
-        // the SGPR file next to the step's own scalars and would spill.
-        const int G = (int)gridDim.x * SL_BITS_WPB, nb = (int)ka.st.B;     // B < 2^31
-        for (int e = (int)b; e < nb; e += G) {
-            auto kp = __builtin_amdgcn_kernarg_segment_ptr();
-            asm volatile("" : "+s"(kp));
-            const StepKArgs &k = *(const StepKArgs *)kp;
-            const int en = e + G < nb ? e + G : -1;
-            step_env<OBS, true>(k.st, k.a, k.fx, e, lane, buf, k.actions, k.ctp, k.ctc,
-                                k.reward_out, k.done_out, k.flags_out, k.ep_len_out, k.ep_rew_out,
-                                pre, en);
-        }
-    } else {
-        step_env<OBS, false>(ka.st, ka.a, ka.fx, b, lane, buf, ka.actions, ka.ctp, ka.ctc,
-                             ka.reward_out, ka.done_out, ka.flags_out, ka.ep_len_out,
-                             ka.ep_rew_out, pre, -1);
-    }
+    step_env<OBS>(ka.st, ka.a, ka.fx, b, lane, buf, ka.actions, ka.ctp, ka.ctc, ka.reward_out,
+                  ka.done_out, ka.flags_out, ka.ep_len_out, ka.ep_rew_out, pre);
 }
 
 // Resets the envs the step kernel queued (one wave per env, grid-stride over the
@@ -737,26 +671,13 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (st.H != N || st.W != N) return SL_ETOOBIG;
-    unsigned grid = (unsigned)((st.B + SL_BITS_WPB - 1) / SL_BITS_WPB);
-    if (SL_BITS_PERSIST) {
-        static int n_cu = 0;           // per process; one device type (gfx950)
-        if (n_cu == 0) {
-            int dev = 0, v = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                v <= 0)
-                v = 256;
-            n_cu = v;
-        }
-        const unsigned cap = (unsigned)(n_cu * SL_BITS_WAVES_PER_CU / SL_BITS_WPB);
-        if (grid > cap) grid = cap;
-    }
+    const unsigned grid = (unsigned)st.B;
     const StepKArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
     if (fx.obs_out) {
         if (fx.obs_vh < 1 || fx.obs_vw < 1 || fx.obs_vh * fx.obs_vw > 4096) return SL_EINVAL;
-        hipLaunchKernelGGL(k_env_step_bits64<true>, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, ka);
+        hipLaunchKernelGGL(k_env_step_bits64<true>, dim3(grid), dim3(64), 0, s, ka);
     } else {
-        hipLaunchKernelGGL(k_env_step_bits64<false>, dim3(grid), dim3(64 * SL_BITS_WPB), 0, s, ka);
+        hipLaunchKernelGGL(k_env_step_bits64<false>, dim3(grid), dim3(64), 0, s, ka);
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);

@@ -36,54 +36,12 @@ using namespace sl::bits;
 
 namespace {
 
-// timing-only ablations (results are wrong when set; never in the shipped build):
-//   1 no start-board load/transpose, 2 no scoring, 4 no board row stores,
-//   8 no board rule
-#ifndef SL_B128_ABL
-#define SL_B128_ABL 0
-#endif
-// phase timing (tuning builds only, -DSL_B128_TIMING=1): s_memtime stamps of every
-// 64th env's wave, read back with sl_debug_phase_times128 (tools/phase_timing128.py)
-#ifndef SL_B128_TIMING
-#define SL_B128_TIMING 0
-#endif
-#if SL_B128_TIMING
-__device__ unsigned long long g_sl_phase128[1024][12];
-#define TM_NOW() ({ __builtin_amdgcn_sched_barrier(0);                                   \
-                    unsigned long long _t = __builtin_amdgcn_s_memtime();                \
-                    __builtin_amdgcn_sched_barrier(0); _t; })
-#define TM_SET(k) tm[k] = TM_NOW()
-#define TM_ACC(k) do { const unsigned long long _n = TM_NOW(); tm[k] += _n - tlast; tlast = _n; } while (0)
-#define TM_MARK() tlast = TM_NOW()
-#else
-#define TM_SET(k)
-#define TM_ACC(k)
-#define TM_MARK()
-#endif
-// Tuning switches; the defaults are the measured best on C5 (MI355X, bench_variants):
-//   PF=1 (next band's rows loaded a band ahead, stores issued behind them): no gain,
-//     the start-board loads queue behind the prefetch (vmcnt is in order);
-//   NOPOOL=0 (start board from the pool's bit planes, DMA'd into LDS at the band's
-//     start, read after the rule): 43.9 vs 38.6 M env-steps/s for NOPOOL=1 (32 HBM
-//     loads + transpose; same box).  Gathering the planes straight from L2 into
-//     registers instead (held across the rule) measured 32.9 vs 37.1;
-//   SEARLY=1: the start board's rows are issued right behind the band's rows, so
-//     they are in flight under the rule.
-#ifndef SL_B128_PF
-#define SL_B128_PF 0
-#endif
-#ifndef SL_B128_NOPOOL
-#define SL_B128_NOPOOL 0
-#endif
-#ifndef SL_B128_SEARLY
-#define SL_B128_SEARLY 1
-#endif
-#ifndef SL_B128_COOP
-#define SL_B128_COOP 0       // spawn draws shared out over the wave (wave_draws)
-#endif
-#ifndef SL_B128_MINW
-#define SL_B128_MINW 2       // waves per SIMD the register budget is sized for
-#endif
+// Measured on C5 (MI355X, round 1): the start board from the pool's bit planes,
+// DMA'd into LDS at the band's start and read after the rule, beat HBM loads +
+// transpose (43.9 vs 38.6 M env-steps/s) and beat gathering the planes from L2 into
+// registers held across the rule (32.9 vs 37.1); prefetching the next band a band
+// ahead gave nothing (the start-board loads queue behind it, vmcnt is in order).
+constexpr int kMinWaves = 2;  // waves per SIMD the register budget is sized for
 
 constexpr int N = 128;       // rows = columns
 constexpr int RS = N / 2;    // dwords per row
@@ -120,12 +78,9 @@ struct GeoBand {
     __device__ __forceinline__ u32 cell_at(int l, int y, int w) const {
         return (u32)((row0 + y) * N + 2 * l + w);
     }
-    DrawLds dl;
-    // spawners are everywhere on the navigation boards: the draws are shared out
     __device__ __forceinline__ void draws(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
                                           u32 tensor) const {
-        if (SL_B128_COOP) wave_draws(*this, elig, sp, sc, tensor, dl, lane);
-        else lane_draws(*this, elig, sp, sc, tensor);
+        lane_draws(*this, elig, sp, sc, tensor);
     }
 };
 
@@ -176,7 +131,7 @@ __device__ __forceinline__ u32 edit_row(u32 d, int r, int ne, const int eidx[4],
 }
 
 // The start-board planes the side-effect term reads (0, 2, 7-15), from the level
-// pool's bit planes when the env was reset from the pool (SL_B128_NOPOOL=0): row y of
+// pool's bit planes when the env was reset from the pool: row y of
 // band t is level row 32t + y - dy, one funnel shift of two adjacent 32-row words;
 // column c is level column c - dx.  At a band's
 // start one global_load_lds per plane copies the two level bands it spans (lanes
@@ -235,7 +190,7 @@ __device__ __forceinline__ const Step128KArgs &kargs128() {
     return *(const Step128KArgs *)kp;
 }
 
-__global__ void __launch_bounds__(64, SL_B128_MINW)
+__global__ void __launch_bounds__(64, kMinWaves)
 k_env_step_bits128(Step128KArgs ka) {
     const sl_env_state &st = ka.st;
     const StepArgs &a = ka.a;
@@ -250,18 +205,9 @@ k_env_step_bits128(Step128KArgs ka) {
     const u32 *gs = reinterpret_cast<const u32 *>(st.start_board + off) + lane;
     u32 *mg = st.planes + b * (int64_t)(NB * MW) + lane;            // mirror [t][q][lane]
 
-#if SL_B128_TIMING
-    unsigned long long tm[12] = {0}, tlast = 0;
-#endif
-    TM_SET(0);
     const u32 V = load_record(st, actions, b, lane);
-    __shared__ uint16_t draw_list[64 * 64];
-#if !SL_B128_NOPOOL
     __shared__ __attribute__((aligned(16))) u32 spool_[kPoolPlanes * 256];
     __attribute__((address_space(3))) u32 *spool = (__attribute__((address_space(3))) u32 *)spool_;
-#endif
-    __shared__ u32 draw_res[128], draw_cnt;
-    const DrawLds dl{(lds_u16_t *)draw_list, (lds_u32_t *)draw_res, (lds_u32_t *)&draw_cnt};
     // pre-step halo rows of every band: above (32t - 1) and below (32t + 32)
     u32 bu[NB], bd[NB];
 #pragma unroll
@@ -271,7 +217,6 @@ k_env_step_bits128(Step128KArgs ka) {
     }
     const int pok = rec(V, R_POK) & 6;
 
-    TM_SET(1);
     SpawnCtx sc;
     sc.gid = a.env0 + (uint32_t)b;
     sc.step = a.step;
@@ -295,7 +240,7 @@ k_env_step_bits128(Step128KArgs ka) {
             load_pairs<RS>(gg + 32 * t * RS, G);
             transpose32(G);
             u32 cg[2];
-            rule_planes(G, cg, GeoBand{lane, 32 * t, HaloView{pick4(gu, t), pick4(gd, t)}, dl}, sc,
+            rule_planes(G, cg, GeoBand{lane, 32 * t, HaloView{pick4(gu, t), pick4(gd, t)}}, sc,
                         1u);
             const u32 rg = wave_or(cg[0] | cg[1]);
             u32 *m = mg + t * MW;       // only the colour planes are ever read back
@@ -317,10 +262,6 @@ k_env_step_bits128(Step128KArgs ka) {
         wait_vm();          // the mirror words are read back below
     }
     __builtin_amdgcn_sched_barrier(0);
-    TM_SET(2);
-
-    u32 Pn[32];                // band 0 in flight under the action
-    if (SL_B128_PF) load_pairs<RS>(gb, Pn);
 
     // ---- the action (lane 0) on the pre-step board
     OverlayT<GlobalCells> ov;
@@ -358,12 +299,11 @@ k_env_step_bits128(Step128KArgs ka) {
         }
     }
 
-    TM_SET(3);
     // ---- board, band by band: rule, scores, changed rows back.  The start board
     // comes from the level pool's planes when the env was reset from the pool
     // (start_roll = (dy << 16) | dx), else from HBM (written by the caller).
     const sl_level_pool &pool = fx.pool;
-    const int roll = (!SL_B128_NOPOOL && pool.board_planes && pool.K > 0 && pool.H == N &&
+    const int roll = (pool.board_planes && pool.K > 0 && pool.H == N &&
                       pool.W == N &&
                       st.start_roll) ? rec(V, R_ROLL) : -1;
     const u32 *pp = reinterpret_cast<const u32 *>(pool.board_planes) +
@@ -371,52 +311,27 @@ k_env_step_bits128(Step128KArgs ka) {
     const int sdy = roll >> 16, sdx = roll & 0xFFFF;
     const int sc0 = (2 * lane - sdx) & (N - 1), sc1 = (sc0 + 1) & (N - 1);
     int pts = 0, scr = 0, pos = 0, side = 0;
-    u32 Dp[32], rbp = 0;       // the previous band's changed rows, stored one band late
 #pragma unroll 1
     for (int t = 0; t < NB; t++) {
         u32 P[32], S[32];
-        TM_MARK();
-        if (SL_B128_PF) {
-#pragma unroll
-            for (int y = 0; y < 32; y++) P[y] = Pn[y];
-            if (t + 1 < NB) load_pairs<RS>(gb + 32 * (t + 1) * RS, Pn);
-            if (rbp) store_pairs<RS>(gb + 32 * (t - 1) * RS, Dp, rbp);
+        load_pairs<RS>(gb + 32 * t * RS, P);
+        if (roll < 0) {
+            load_pairs<RS>(gs + 32 * t * RS, S);      // in flight under the rule
         } else {
-            load_pairs<RS>(gb + 32 * t * RS, P);
-            if (SL_B128_SEARLY && roll < 0 && !(SL_B128_ABL & 1)) load_pairs<RS>(gs + 32 * t * RS, S);
-        }
-#if !SL_B128_NOPOOL
-        if (roll >= 0 && !(SL_B128_ABL & 1)) {
             wait_lgkm();        // the previous band's reads of the buffer are done
             pool_dma128(pp, t, sdy, lane, spool);
         }
-#endif
         transpose32(P);
         const u32 erow = apply_edits(P, ne, eidx, eval, 32 * t, lane);
-        TM_ACC(4);
         u32 cb[2];
-        if (SL_B128_ABL & 8) {
-            cb[0] = PL(P, 0, 0) & 1u;
-            cb[1] = 0u;
-        } else {
-            rule_planes(P, cb, GeoBand{lane, 32 * t, HaloView{pick4(bu, t), pick4(bd, t)}, dl},
-                        sc, 0u);
-        }
+        rule_planes(P, cb, GeoBand{lane, 32 * t, HaloView{pick4(bu, t), pick4(bd, t)}}, sc, 0u);
         __builtin_amdgcn_sched_barrier(0);
-        TM_ACC(5);
-        if (SL_B128_ABL & 1) {
-#pragma unroll
-            for (int y = 0; y < 32; y++) S[y] = P[y];
-        } else if (roll < 0) {
-            if (!(SL_B128_SEARLY && !SL_B128_PF)) load_pairs<RS>(gs + 32 * t * RS, S);
+        if (roll < 0) {
             transpose32(S);
         } else {
-#if !SL_B128_NOPOOL
             wait_vm();          // the band's pool planes have landed in LDS
             pool_start_lds(spool, t, sdy, sc0, sc1, S);
-#endif
         }
-        TM_ACC(6);
         u32 gcol[3][2];
         const u32 *m = mg + t * MW;
 #pragma unroll
@@ -425,37 +340,20 @@ k_env_step_bits128(Step128KArgs ka) {
             gcol[k][1] = m[(25 + k) * 64];
         }
         int p, q, r, e;
-        if (SL_B128_ABL & 2) {
-            p = PL(P, 3, 0) & 3;
-            q = PL(S, 5, 1) & 1;
-            r = gcol[0][1] & 1;
-            e = 0;
-        } else {
-            score_planes(P, gcol, S, &p, &q, &r, &e);
-        }
+        score_planes(P, gcol, S, &p, &q, &r, &e);
         pts += p;
         scr += q;
         pos += r;
         side += e;
         const u32 rb = wave_or(cb[0] | cb[1]) | erow;
-        TM_ACC(7);
-        if (rb && !(SL_B128_ABL & 4)) {
+        if (rb) {
             transpose32(P);
-            if (SL_B128_PF) {
-#pragma unroll
-                for (int y = 0; y < 32; y++) Dp[y] = P[y];
-            } else {
-                store_pairs<RS>(gb + 32 * t * RS, P, rb);
-            }
+            store_pairs<RS>(gb + 32 * t * RS, P, rb);
         }
-        rbp = (SL_B128_ABL & 4) ? 0u : rb;
-        TM_ACC(8);
     }
-    if (SL_B128_PF && rbp) store_pairs<RS>(gb + 32 * (NB - 1) * RS, Dp, rbp);
     const int points = wave_total(pts), score = wave_total(scr);
     const int possible = wave_total(pos), side_total = wave_total(side);
     wait_vm();              // row stores land before the epilogue rewrites the exits
-    TM_SET(9);
     if (lane == 0) {
         const Step128KArgs &k = kargs128();
         const bool reset = epilogue_core(k.st, k.a, b, fl, act_reward, points, score, possible,
@@ -467,23 +365,11 @@ k_env_step_bits128(Step128KArgs ka) {
             reinterpret_cast<int32_t *>(k.fx.scratch + 2 * k.st.B)[i] = (int32_t)b;
         }
     }
-#if SL_B128_TIMING
-    TM_SET(10);
-    if ((b & 63) == 0 && lane == 0)
-        for (int k = 0; k < 12; k++) g_sl_phase128[(b >> 6) & 1023][k] = tm[k];
-#endif
 }
 
 }  // namespace
 
 namespace sl {
-
-#if SL_B128_TIMING
-extern "C" int sl_debug_phase_times128(unsigned long long *host) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sl_phase128), sizeof(g_sl_phase128)) ==
-                   hipSuccess ? 0 : -1;
-}
-#endif
 
 bool bits128_shape(const sl_env_state &st) {
     return st.H == N && st.W == N && st.planes && st.planes_ok;

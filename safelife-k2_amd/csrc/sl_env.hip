@@ -819,7 +819,12 @@ int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, co
 }
 }  // namespace sl
 
-extern "C" const char *sl_version(void) { return "safelife-hip 0.1 (gfx950)"; }
+extern "C" const char *sl_version(void) { return "safelife-hip 0.2 (gfx950)"; }
+
+#ifndef SL_BUILD_ID
+#define SL_BUILD_ID "unknown"
+#endif
+extern "C" const char *sl_build_id(void) { return SL_BUILD_ID; }
 
 extern "C" int sl_device_arch(char *buf, int len) {
     int dev;
@@ -880,7 +885,9 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     if (!state_ok(st) || !cfg || !actions || !reward || !done || !cfg->scratch) return SL_EINVAL;
     if (cfg->bonus_period < 0 || cfg->bonus_period > SL_BONUS_PERIOD_MAX) return SL_EINVAL;
     if (cfg->bonus_period > 0 && (!cfg->bonus_table || cfg->bonus_len < 1)) return SL_EINVAL;
-    if (cfg->auto_reset && (!pool || !info_flags)) return SL_EINVAL;
+    if (cfg->auto_reset && (!pool || !info_flags || pool->K <= 0 || pool->H != st->H ||
+                            pool->W != st->W))
+        return SL_EINVAL;
     const int64_t B = st->B;
     if (B == 0) return SL_OK;
     hipStream_t s = (hipStream_t)stream;
@@ -901,7 +908,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     a.n_draws = cfg->n_draws;
 
     const bool philox_fast = cfg->rng_mode == SL_RNG_PHILOX && cfg->kernel != SL_KERNEL_GENERIC;
-    const bool fast = philox_fast && fast_shape(st->H, st->W);
+    const bool fast = philox_fast && st->H == 64 && st->W == 64;
     const bool fast128 = philox_fast && bits128_shape(*st);
     const bool small = philox_fast && !fast && small_shape(*st);
     if (cfg->kernel == SL_KERNEL_FAST && !fast && !fast128 && !small) return SL_ETOOBIG;
@@ -921,7 +928,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         if (rc) return rc;
     }
     const bool fuse_obs = cfg->obs_out && fast && oa.mode == SL_OBS_PACKED &&
-                          oa.vh * oa.vw <= kObsMaxCells && launch_fast_fuses_obs();
+                          oa.vh * oa.vw <= kObsMaxCells;
     fx.obs_out = fuse_obs ? (uint16_t *)cfg->obs_out : nullptr;
     fx.obs_vh = cfg->obs_vh;
     fx.obs_vw = cfg->obs_vw;
@@ -942,11 +949,11 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         reset_done = fx.fuse_reset && fx.pool.K > 0 && fx.pool.H == st->H && fx.pool.W == st->W;
     } else if (fast) {
         if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
-        int rc = launch_step_fast(*st, a, fx, actions, cfg->can_toggle_powers,
+        int rc = launch_step_bits(*st, a, fx, actions, cfg->can_toggle_powers,
                                   cfg->can_toggle_colors, reward, done, info_flags, ep_len,
                                   ep_reward, s);
         if (rc) return rc;
-        reset_done = launch_fast_fuses_reset(*st, fx);
+        reset_done = fx.fuse_reset && fx.pool.K > 0;
     } else {
         hipLaunchKernelGGL(k_env_action, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, *st,
                            actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act);

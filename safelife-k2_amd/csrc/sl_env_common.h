@@ -234,7 +234,7 @@ __device__ __forceinline__ uint16_t reset_scalars(const sl_env_state &st,
     return (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
 }
 
-// fused fast path (sl_fast.hip / sl_bits.hip): action + advance + scores (+ reset)
+// fused bit-sliced paths (sl_bits*.hip): action + advance + scores (+ reset)
 struct FastExtra {
     sl_level_pool pool;     // K == 0: no pool given
     ResetArgs ra;
@@ -246,13 +246,6 @@ struct FastExtra {
     uint16_t *obs_out;      // 64x64 kernel: packed views written from the on-chip
     int32_t obs_vh, obs_vw, obs_rw;   // board (NULL: none); view shape, remove_white
 };
-bool fast_shape(int H, int W);
-int launch_step_fast(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
-                     const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
-                     uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
-// true when the launched fast kernel also performed the auto-resets
-bool launch_fast_fuses_reset(const sl_env_state &st, const FastExtra &fx);
-bool launch_fast_fuses_obs();
 // bit-sliced 128x128 kernel (sl_bits128.hip); needs the goals mirror (st.planes).
 // With fx.fuse_reset it queues the envs that finished and launches
 // k_env_reset_list_wide for them.

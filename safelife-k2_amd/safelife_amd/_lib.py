@@ -89,6 +89,7 @@ def lib():
             "path has no CPU fallback" % (LIB_PATH, CSRC))
     L = ctypes.CDLL(LIB_PATH)
     L.sl_version.restype = ctypes.c_char_p
+    L.sl_build_id.restype = ctypes.c_char_p
     L.sl_device_arch.argtypes = [ctypes.c_char_p, ctypes.c_int]
     L.sl_advance.argtypes = [vp, vp, i64, ctypes.c_int, ctypes.c_int, vp, f32, ctypes.c_int,
                              u64, u32, u32, u32, vp, vp, vp]
@@ -142,3 +143,8 @@ def stream_ptr(device):
 
 def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def build_id():
+    """Hash of the sources the loaded library was built from (Makefile BUILD_ID)."""
+    return lib().sl_build_id().decode()

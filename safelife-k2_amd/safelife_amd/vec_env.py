@@ -33,7 +33,14 @@ ACTION_NAMES = ("NULL", "MOVE UP", "MOVE RIGHT", "MOVE DOWN", "MOVE LEFT",
 
 
 class GlobalCounter:
-    """Host mirror of SafeLifeEnv.global_counter (safelife_env.py:81-85)."""
+    """Host mirror of SafeLifeEnv.global_counter (safelife_env.py:81-85).
+
+    ``num_steps`` is added on the host at every step (it drives the wrapper
+    schedules, env_wrappers.py:29-36).  Episode starts and completions happen inside
+    the step kernels (auto-reset), so a vector env folds them in from its device
+    counters at logging cadence: :meth:`SafeLifeVecEnv.sync_counters` (one sync).
+    One counter may be shared by several envs, like the reference's class-level one.
+    """
 
     def __init__(self):
         self.episodes_started = 0
@@ -88,6 +95,12 @@ class SafeLifeVecEnv:
                        "fast": _lib.SL_KERNEL_FAST}[kernel]
         self.global_counter = global_counter if global_counter is not None else GlobalCounter()
         self._step_index = 0
+        # step index and auto_reset flag of the last launched step: the 64x64 and
+        # 128x128 kernels queue finished envs in per-parity lists (sl_env_cfg.scratch)
+        # that are valid only for consecutive auto-reset steps
+        self._last_step = None
+        self._abandoned = 0          # explicit resets of episodes that had not ended
+        self._synced = (0, 0)        # (started, completed) already in global_counter
         self._alloc(obs_dtype)
         if rng == "stream":
             if spawn_stream is None:
@@ -157,14 +170,20 @@ class SafeLifeVecEnv:
         self._pool_dev = self.pool.to_device(self.device)
         self._cfg = _lib.EnvCfg()
 
-    def set_pool(self, levels):
-        """Replace the level pool the next resets draw from (same board shape)."""
+    def set_pool(self, levels, pool_dev=None):
+        """Replace the level pool the next resets draw from (same board shape).
+
+        ``pool_dev`` is an already uploaded ``levels.to_device(...)`` (see
+        :class:`safelife_amd.pool_feed.PoolFeeder`, which uploads on a side stream);
+        the swap itself is stream-ordered and does not synchronise the host."""
         pool = levels if isinstance(levels, LevelPool) else LevelPool.from_levels(levels)
         if (pool.H, pool.W) != (self.H, self.W):
             raise ValueError("pool boards are %dx%d, the env's %dx%d"
                              % (pool.H, pool.W, self.H, self.W))
+        if pool.K < 1:
+            raise ValueError("empty level pool")
         self.pool = pool
-        self._pool_dev = pool.to_device(self.device)
+        self._pool_dev = pool_dev if pool_dev is not None else pool.to_device(self.device)
         # running episodes' start boards are no longer levels of the pool: the
         # kernels read them from HBM until those envs are reset from the new pool
         self.st_t["start_roll"].fill_(-1)
@@ -228,12 +247,41 @@ class SafeLifeVecEnv:
         m = None
         if mask is not None:
             m = self.torch.as_tensor(mask, device=self.device).to(self.torch.uint8).contiguous()
+            if m.numel() != self.B:
+                raise ValueError("reset mask must have %d entries" % self.B)
+        # episodes cut short by this reset were started but never completed
+        # (SafeLifeEnv.step counts a completion only when an episode ends)
+        running = self._running_mask()
+        if m is not None:
+            running = running & (m.reshape(self.B) != 0)
+        self._abandoned += int(running.sum().item())
         _lib.check(L.sl_env_reset(ctypes.byref(self._state), ctypes.byref(self._pool_dev["struct"]),
                                   _lib.ptr(m), ctypes.byref(cfg), _lib.stream_ptr(self.device)),
                    "sl_env_reset")
-        self.global_counter.episodes_started += self.B if mask is None else int(
-            self.torch.count_nonzero(m).item())
+        self.sync_counters()
         return self.observe() if self.compute_obs else None
+
+    def _running_mask(self):
+        """Envs inside an episode that has not ended (started, neither game over nor
+        past the time limit: safelife_env.py:167-168)."""
+        st = self.st_t
+        ended = (st["game_over"] != 0) | (st["episode_length"] > self.time_limit)
+        return (st["episodes"] > 0) & ~ended
+
+    def sync_counters(self):
+        """Fold the episodes started / completed since the last call into
+        ``global_counter`` (one device sync; call at logging cadence).
+
+        Every reset, explicit or automatic, bumps the env's device episode count;
+        an episode is completed unless it is still running or was cut short by an
+        explicit reset."""
+        started = int(self.st_t["episodes"].sum().item())
+        completed = started - int(self._running_mask().sum().item()) - self._abandoned
+        s0, c0 = self._synced
+        self.global_counter.episodes_started += started - s0
+        self.global_counter.episodes_completed += completed - c0
+        self._synced = (started, completed)
+        return self.global_counter
 
     def observe(self, out=None):
         """Write the observations into `out` (a tensor shaped and typed like
@@ -277,6 +325,7 @@ class SafeLifeVecEnv:
         self._actions_in_flight = a
         L = _lib.lib()
         cfg = self._fill_cfg()
+        self._check_reset_lists()
         # the observation is written by sl_env_step itself (from the on-chip board
         # where the kernel allows it)
         obs = None
@@ -294,6 +343,17 @@ class SafeLifeVecEnv:
                    "sl_env_step")
         self._step_index += 1
         self.global_counter.num_steps += self.B
+
+    def _check_reset_lists(self):
+        """Zero the per-parity reset-list lengths (scratch[8B+2 : 8B+4]) unless this
+        step directly follows an auto-reset step: each step's reset kernel zeroes
+        only the other parity's list (sl_env_common.h, Scratch)."""
+        cur = (self._step_index, self.auto_reset)
+        last = self._last_step
+        if not (self.auto_reset and last is not None and last[1]
+                and last[0] + 1 == self._step_index):
+            self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()
+        self._last_step = cur
 
     def _fill_obs_cfg(self, cfg, out):
         cfg.obs_out = None if out is None else out.data_ptr()
@@ -343,13 +403,22 @@ class SafeLifeVecEnv:
         torch = self.torch
         for dst, src in ((self.board, board), (self.goals, goals), (self.start_board, start_board)):
             dst.copy_(torch.as_tensor(np.ascontiguousarray(src, dtype=np.uint16)).to(self.device))
-        # the start board no longer matches a pool level: kernels read it from HBM;
-        # the bit-plane mirrors are stale
-        self.st_t["start_roll"].fill_(-1)
-        self.planes_ok.zero_()
         for k, v in scalars.items():
             t = self.st_t[k]
             t.copy_(torch.as_tensor(np.asarray(v)).to(device=self.device, dtype=t.dtype))
+        self._invalidate_caches()
+
+    def _invalidate_caches(self):
+        """After state was written from outside the kernels: the start boards no
+        longer match pool levels (kernels read them from HBM), the bit-plane
+        mirrors are stale and the reset lists start empty."""
+        self.st_t["start_roll"].fill_(-1)
+        self.planes_ok.zero_()
+        self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()
+        self._last_step = None
+        self._synced = (int(self.st_t["episodes"].sum().item()),
+                        int(self.st_t["episodes"].sum().item())
+                        - int(self._running_mask().sum().item()) - self._abandoned)
 
     def state_dict(self):
         d = {"board": self.board.clone(), "goals": self.goals.clone(),
@@ -359,7 +428,12 @@ class SafeLifeVecEnv:
         return d
 
     def load_state_dict(self, d):
-        self.planes_ok.zero_()             # mirrors are rebuilt by the next step
+        """Restore a state_dict().  Level indices must address the current pool
+        (the start boards themselves are restored from the dict and read from HBM)."""
+        li = d["level_index"]
+        if int(li.min().item()) < 0 or int(li.max().item()) >= self.pool.K:
+            raise ValueError("state_dict level_index outside the current pool of %d levels"
+                             % self.pool.K)
         self.board.copy_(d["board"])
         self.goals.copy_(d["goals"])
         self.start_board.copy_(d["start_board"])
@@ -367,3 +441,4 @@ class SafeLifeVecEnv:
             v.copy_(d[k])
         self._step_index = int(d["step_index"])
         self.stream_pos.copy_(d["stream_pos"])
+        self._invalidate_caches()

@@ -4,8 +4,9 @@
 Usage: keep_profile.py <gpurun_out/name> <tag> [--pmc-config c3]
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
   profiles/<tag>_summary.json       per-kernel averages (all launches and timed window)
-  profiles/pmc_<config>.json        HBM bytes per launch of the step kernel (bench.py
-                                    reads it for roofline.traffic when the kernel matches)
+  profiles/pmc_<config>.json        HBM bytes per launch of the step kernel, keyed on the
+                                    library's build id (bench.py reads it for
+                                    roofline.traffic only when the build matches)
 """
 import glob
 import json
@@ -30,7 +31,10 @@ def main(src, tag, cfg=None):
         k = step[0]
         d = summ["kernels"][k]
         lk = d.get("last_k", {})
-        rec = {"kernel": k, "profile": tag,
+        bid_path = os.path.join(REPO, "safelife-k2_amd", "safelife_amd", "_native",
+                                "build_id.txt")
+        bid = open(bid_path).read().strip() if os.path.exists(bid_path) else None
+        rec = {"kernel": k, "profile": tag, "build_id": bid,
                "hbm_bytes_per_launch": lk.get("hbm_bytes_per_launch", d.get("hbm_bytes_per_launch")),
                "hbm_read_bytes": lk.get("hbm_read_bytes", d.get("hbm_read_bytes")),
                "hbm_write_bytes": lk.get("hbm_write_bytes", d.get("hbm_write_bytes")),

@@ -10,7 +10,7 @@ OUT=$R/gpurun_out/$NAME
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 STEPS=200
-BENCH="$R/bench.py --steps $STEPS --warmup 20 --no-cpu-baseline $*"
+BENCH="$R/bench.py --steps $STEPS --warmup 20 --no-cpu-baseline --pmc off $*"
 run() {  # name, rocprof args...
   local n=$1; shift
   timeout -k 10 400 rocprofv3 "$@" --output-format csv -d $OUT/$n -o $n -- python3 $BENCH > $OUT/$n.log 2>&1
