@@ -133,6 +133,22 @@ int sl_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n,
  * max_keys <= 1024.  The earth mover's distance over the maps
  * (side_effects.py:12-56, third-party pyemd) is host code above this call.
  */
+/*
+ * Earth mover's distance of side_effect_score (host code; no GPU needed).
+ * Replaces pyemd.emd(a[changed], b[changed], dist, extra_mass_penalty) at
+ * /root/reference/safelife/side_effects.py:56 (its caller's cell selection and
+ * ground distance: side_effects.py:36-55).
+ *   p, q         host double [n]: the two densities at the n selected cells
+ *   ys, xs       host int32 [n]: the cells' row / column on an H x W board
+ *   cost_table   host double [2H-1][2W-1]: ground distance between two cells by their
+ *                signed offset (y_i - y_j + H - 1, x_i - x_j + W - 1)
+ *   extra_mass_penalty  per unit of |sum p - sum q|; -1: the largest distance used
+ *   out          the distance (FastEMD emd_hat semantics, see sl_emd.cpp)
+ */
+int sl_emd_cells(const double *p, const double *q, const int32_t *ys, const int32_t *xs,
+                 int64_t n, const double *cost_table, int H, int W,
+                 double extra_mass_penalty, double *out);
+
 int sl_side_effect_workspace(int64_t E, int H, int W, int64_t *bytes);
 int sl_side_effect_densities(const uint16_t *init_board, const uint16_t *final_board,
                              const int32_t *num_steps_dev, const int32_t *num_steps_host,

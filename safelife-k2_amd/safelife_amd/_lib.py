@@ -109,13 +109,15 @@ def lib():
     L.sl_sample_actions.argtypes = [vp, ctypes.c_int, i64, ctypes.c_int, i64, ctypes.c_int, vp,
                                     u64, u32, u32, f64, vp, vp, vp]
     L.sl_gae.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, i64, f64, vp, vp, vp]
+    L.sl_emd_cells.argtypes = [vp, vp, vp, vp, i64, vp, ctypes.c_int, ctypes.c_int, f64,
+                               ctypes.POINTER(f64)]
     L.sl_event_create.argtypes = [ctypes.POINTER(vp)]
     L.sl_event_destroy.argtypes = [vp]
     L.sl_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(f32)]
     for name in ("sl_event_create", "sl_event_destroy", "sl_event_elapsed_ms", "sl_device_arch", "sl_advance", "sl_count_eligible", "sl_exclusive_scan_i64",
                  "sl_env_step", "sl_env_reset", "sl_env_obs", "sl_level_pool_prepare",
                  "sl_side_effect_workspace", "sl_side_effect_densities",
-                 "sl_sample_actions", "sl_gae"):
+                 "sl_sample_actions", "sl_gae", "sl_emd_cells"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

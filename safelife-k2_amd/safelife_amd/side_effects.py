@@ -10,8 +10,9 @@ action (b1) runs.
 
 ``earth_mover_distance`` / ``side_effect_score`` complete the reference API on the
 host, as the reference itself does (numpy + the third-party ``pyemd``, which is
-absent here).  The EMD is solved as the exact transport linear program of
-EMD-hat (Pele & Werman; what ``pyemd.emd`` computes) with scipy's HiGHS solver.
+absent here).  The EMD is FastEMD's emd_hat (what ``pyemd.emd`` computes), solved
+exactly by a transportation simplex in host C++ (``sl_emd_cells``,
+csrc/sl_emd.cpp) over a per-offset ground-distance table.
 Parity unpinned: no pyemd output exists in this environment to compare against.
 """
 import ctypes
@@ -93,56 +94,69 @@ def side_effect_densities(init_boards, final_boards, num_steps, spawn_prob, num_
     return out
 
 
+def ground_distance_table(H, W, metric="manhattan", wrap_x=True, wrap_y=True, tanh_scale=5.0):
+    """Ground distance between two cells of an H x W board as a function of their
+    signed offset: entry [dy + H - 1, dx + W - 1] for dy = y_i - y_j, dx = x_i - x_j.
+
+    These are the values side_effects.py:44-55 forms pairwise: a wrap replaces an
+    offset d by min(d, size - d), which shortens positive offsets only (negative ones
+    pass through unchanged), so the distance is not symmetric; then Manhattan or
+    Euclidean length, then tanh(d / tanh_scale) when tanh_scale > 0.  Integer
+    offsets, float64 results, the same numpy operations."""
+    dy = np.arange(1 - H, H, dtype=np.int64)[:, None]
+    dx = np.arange(1 - W, W, dtype=np.int64)[None, :]
+    if wrap_x:
+        dx = np.minimum(dx, W - dx)
+    if wrap_y:
+        dy = np.minimum(dy, H - dy)
+    dy, dx = np.broadcast_arrays(dy, dx)
+    if metric == "manhattan":
+        d = (np.abs(dx) + np.abs(dy)).astype(float)
+    else:
+        d = np.sqrt(dx * dx + dy * dy)
+    if tanh_scale > 0:
+        d = np.tanh(d / tanh_scale)
+    return np.ascontiguousarray(d, dtype=np.float64)
+
+
+def emd_cells(p, q, ys, xs, table, extra_mass_penalty=1.0):
+    """EMD between masses p and q on the cells (ys, xs) under a ground-distance
+    table (ground_distance_table): the exact transport of sl_emd_cells (host C++,
+    FastEMD's emd_hat semantics: pre-flow, 1e6 fixed point, extra-mass penalty)."""
+    L = _lib.lib()
+    p = np.ascontiguousarray(p, dtype=np.float64)
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    ys = np.ascontiguousarray(ys, dtype=np.int32)
+    xs = np.ascontiguousarray(xs, dtype=np.int32)
+    table = np.ascontiguousarray(table, dtype=np.float64)
+    n = p.shape[0]
+    if not (q.shape == ys.shape == xs.shape == (n,)) or table.ndim != 2:
+        raise ValueError("p, q, ys, xs must be [n]; table [2H-1, 2W-1]")
+    H, W = (table.shape[0] + 1) // 2, (table.shape[1] + 1) // 2
+    out = ctypes.c_double()
+    _lib.check(L.sl_emd_cells(p.ctypes.data, q.ctypes.data, ys.ctypes.data, xs.ctypes.data, n,
+                              table.ctypes.data, H, W, float(extra_mass_penalty),
+                              ctypes.byref(out)), "sl_emd_cells")
+    return out.value
+
+
 def earth_mover_distance(a, b, metric="manhattan", wrap_x=True, wrap_y=True, tanh_scale=5.0,
                          extra_mass_penalty=1.0):
-    """side_effects.py:12-56: EMD between two 2-d distributions over the cells where
-    they differ, with the reference's (one-sided) wrapped Manhattan/Euclidean ground
-    distance.  Parity unpinned (pyemd is not installed here)."""
-    from scipy.optimize import linprog
-    a = np.asanyarray(a, dtype=float)
-    b = np.asanyarray(b, dtype=float)
-    x, y = np.meshgrid(np.arange(a.shape[1]), np.arange(a.shape[0]))
-    delta = np.abs(a - b)
-    changed = delta > 1e-3 * np.max(delta)
-    if not changed.any():
+    """side_effects.py:12-56 (same signature and result convention): the EMD between
+    two 2-d densities, restricted to the cells where they differ by more than 1e-3 of
+    the largest difference, under the reference's ground distance.  The transport
+    runs in host C++ (sl_emd_cells).  Parity unpinned (pyemd is not installed)."""
+    a = np.asarray(a, dtype=float)
+    b = np.asarray(b, dtype=float)
+    if a.shape != b.shape or a.ndim != 2:
+        raise ValueError("a and b must be 2-d arrays of one shape")
+    gap = np.abs(a - b)
+    sel = gap > 1e-3 * np.max(gap)
+    if not sel.any():
         return 0.0
-    dx = np.subtract.outer(x[changed], x[changed])
-    dy = np.subtract.outer(y[changed], y[changed])
-    if wrap_x:
-        dx = np.minimum(dx, a.shape[1] - dx)
-    if wrap_y:
-        dy = np.minimum(dy, a.shape[0] - dy)
-    if metric == "manhattan":
-        dist = (np.abs(dx) + np.abs(dy)).astype(float)
-    else:
-        dist = np.sqrt(dx * dx + dy * dy)
-    if tanh_scale > 0:
-        dist = np.tanh(dist / tanh_scale)
-    return emd_hat(a[changed], b[changed], dist, extra_mass_penalty)
-
-
-def emd_hat(p, q, dist, extra_mass_penalty=-1.0):
-    """EMD-hat (the quantity pyemd.emd returns): the cheapest transport of
-    min(sum p, sum q) mass from p to q under ``dist`` plus |sum p - sum q| times the
-    extra-mass penalty (negative: the largest ground distance).  Exact LP (HiGHS)."""
-    from scipy.optimize import linprog
-    p = np.asarray(p, dtype=float)
-    q = np.asarray(q, dtype=float)
-    n, m = len(p), len(q)
-    if extra_mass_penalty < 0:
-        extra_mass_penalty = float(np.max(dist)) if dist.size else 0.0
-    flow = min(p.sum(), q.sum())
-    a_ub = np.zeros((n + m, n * m))
-    for i in range(n):
-        a_ub[i, i * m:(i + 1) * m] = 1.0
-    for j in range(m):
-        a_ub[n + j, j::m] = 1.0
-    res = linprog(np.asarray(dist, dtype=float).ravel(), A_ub=a_ub,
-                  b_ub=np.concatenate([p, q]), A_eq=np.ones((1, n * m)), b_eq=[flow],
-                  bounds=(0, None), method="highs")
-    if not res.success:
-        raise RuntimeError("EMD transport LP failed: %s" % res.message)
-    return float(res.fun) + abs(p.sum() - q.sum()) * extra_mass_penalty
+    ys, xs = np.nonzero(sel)                 # row-major: the reference's bin order
+    table = ground_distance_table(a.shape[0], a.shape[1], metric, wrap_x, wrap_y, tanh_scale)
+    return emd_cells(a[sel], b[sel], ys, xs, table, extra_mass_penalty)
 
 
 def side_effect_score(game, num_samples=1000, include=None, exclude=None, **kw):

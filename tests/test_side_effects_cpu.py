@@ -1,27 +1,143 @@
-"""Host-side EMD of side_effect_score (side_effects.py:12-56) -- known answers.
+"""Host-side EMD of side_effect_score (side_effects.py:12-56), CPU only.
 
-Parity with pyemd itself is unpinned (pyemd is not installed); these pin the
-transport problem EMD-hat defines."""
+The transport runs in the C ABI's host code (sl_emd_cells, csrc/sl_emd.cpp), which
+restates pyemd 0.5.1's emd (FastEMD emd_hat_gd_metric on doubles: pre-flow, 1e6
+fixed point, extra-mass penalty).  Parity with pyemd itself is unpinned (pyemd is
+not installed); these tests pin the semantics the reference's call implies and
+check the solver's optimum against independent exact solvers (scipy's HiGHS LP and
+linear_sum_assignment) on the same fixed-point problem."""
+import time
+
 import numpy as np
+import pytest
 
-from safelife_amd.side_effects import emd_hat, earth_mover_distance
-
-
-def test_emd_hat_known_answers():
-    d = np.array([[0.0, 2.0], [2.0, 0.0]])
-    assert emd_hat([1.0, 0.0], [1.0, 0.0], d) == 0.0
-    assert abs(emd_hat([1.0, 0.0], [0.0, 1.0], d) - 2.0) < 1e-12
-    # half the mass moves, half is extra (penalty 1.0)
-    assert abs(emd_hat([1.0, 0.0], [0.0, 0.5], d, 1.0) - (0.5 * 2.0 + 0.5)) < 1e-12
-    # negative penalty -> the largest ground distance
-    assert abs(emd_hat([1.0], [0.25], np.zeros((1, 1)), -1.0) - 0.0) < 1e-12
+from safelife_amd.side_effects import (earth_mover_distance, emd_cells,
+                                       ground_distance_table)
 
 
-def test_earth_mover_distance_grid():
+def _quantised_lp(p, q, ys, xs, table, penalty):
+    """The same fixed-point problem solved by HiGHS: returns the EMD."""
+    from scipy.optimize import linprog
+    H, W = (table.shape[0] + 1) // 2, (table.shape[1] + 1) // 2
+    p, q = np.array(p, float), np.array(q, float)
+    m = np.minimum(p, q)
+    p, q = p - m, q - m                              # pre-flow
+    C = table[ys[:, None] - ys[None, :] + H - 1, xs[:, None] - xs[None, :] + W - 1]
+    maxC = C.max()
+    maxs, mins = max(p.sum(), q.sum()), min(p.sum(), q.sum())
+    if maxC <= 0 or maxs <= 0:
+        return (maxs - mins) * penalty
+    pq, cn = 1e6 / maxs, 1e6 / maxC
+    ip, iq = np.floor(p * pq + 0.5), np.floor(q * pq + 0.5)
+    ic = np.floor(C * cn + 0.5)
+    if iq.sum() > ip.sum():
+        ip, iq = iq, ip                              # C kept as given (not transposed)
+    si, dj = np.nonzero(ip)[0], np.nonzero(iq)[0]
+    cost = ic[np.ix_(si, dj)]
+    n, k = len(si), len(dj)
+    a_ub = np.zeros((n, n * k))
+    for r in range(n):
+        a_ub[r, r * k:(r + 1) * k] = 1
+    a_eq = np.zeros((k, n * k))
+    for c in range(k):
+        a_eq[c, c::k] = 1
+    res = linprog(cost.ravel(), A_ub=a_ub, b_ub=ip[si], A_eq=a_eq, b_eq=iq[dj],
+                  bounds=(0, None), method="highs")
+    assert res.success
+    return round(res.fun) / pq / cn + (maxs - mins) * penalty
+
+
+def test_known_answers():
     a = np.zeros((8, 8))
     b = np.zeros((8, 8))
     assert earth_mover_distance(a, b) == 0.0
     a[2, 2] = 1.0
     b[2, 4] = 1.0
-    # manhattan distance 2, tanh(2 / 5)
+    # Manhattan distance 2, tanh(2 / 5)
     assert abs(earth_mover_distance(a, b) - np.tanh(2 / 5.0)) < 1e-9
+    assert abs(earth_mover_distance(a, b, tanh_scale=0) - 2.0) < 1e-9
+    assert abs(earth_mover_distance(a, b, metric="euclidean", tanh_scale=0) - 2.0) < 1e-9
+    # extra mass: 2 units against 1, penalty 1 per unit
+    a[2, 2] = 2.0
+    assert abs(earth_mover_distance(a, b, tanh_scale=0) - (2.0 + 1.0)) < 1e-9
+    assert abs(earth_mover_distance(a, b, tanh_scale=0, extra_mass_penalty=0.0) - 2.0) < 1e-9
+
+
+def test_one_sided_wrap():
+    """side_effects.py:46-49 wraps with min(d, size - d) on the signed offset
+    x_i - x_j, which shortens positive offsets only: moving mass from column 7 to
+    column 0 of an 8-wide board costs 1, from column 0 to column 7 costs 7."""
+    a, b = np.zeros((4, 8)), np.zeros((4, 8))
+    a[1, 7], b[1, 0] = 1.0, 1.0
+    # costs are rounded to 1e-6 of the largest pairwise distance (7 here): FastEMD's
+    # fixed point, so 1 comes back as 142857 / (1e6 / 7)
+    assert abs(earth_mover_distance(a, b, tanh_scale=0) - 1.0) < 1e-6 * 7
+    assert earth_mover_distance(a, b, tanh_scale=0) == 142857 / (1e6 / 7)
+    assert abs(earth_mover_distance(b, a, tanh_scale=0) - 7.0) < 1e-9
+    assert abs(earth_mover_distance(b, a, tanh_scale=0, wrap_x=False) - 7.0) < 1e-9
+    t = ground_distance_table(4, 8, tanh_scale=0)
+    assert t[3, 7 + 7] == 1.0 and t[3, 7 - 7] == 7.0
+
+
+def test_degenerate_inputs():
+    t = ground_distance_table(5, 5)
+    assert emd_cells([], [], [], [], t) == 0.0
+    # one cell: zero distance, the extra mass alone
+    assert abs(emd_cells([3.0], [1.0], [2], [2], t, 1.0) - 2.0) < 1e-12
+    with pytest.raises(RuntimeError):
+        emd_cells([1.0], [0.0], [7], [0], t)          # outside the board
+
+
+@pytest.mark.parametrize("seed,n,metric", [(0, 12, "manhattan"), (1, 30, "euclidean"),
+                                           (2, 45, "manhattan"), (3, 80, "manhattan")])
+def test_matches_exact_lp(seed, n, metric):
+    rng = np.random.RandomState(seed)
+    H, W = 16, 20
+    cells = rng.choice(H * W, size=n, replace=False)
+    ys, xs = cells // W, cells % W
+    p = rng.rand(n) * (rng.rand(n) < 0.6)
+    q = rng.rand(n) * (rng.rand(n) < 0.6)
+    t = ground_distance_table(H, W, metric, tanh_scale=5.0 if seed % 2 == 0 else 0)
+    for penalty in (1.0, -1.0, 0.25):
+        got = emd_cells(p, q, ys, xs, t, penalty)
+        pen = penalty if penalty != -1.0 else t[ys[:, None] - ys[None, :] + H - 1,
+                                                xs[:, None] - xs[None, :] + W - 1].max()
+        ref = _quantised_lp(p, q, ys, xs, t, pen)
+        assert abs(got - ref) <= 1e-9 * max(1.0, abs(ref)), (penalty, got, ref)
+
+
+def test_large_assignment_instance():
+    """2 000 changed cells of a 64x64 board, 1 000 unit sources and 1 000 unit sinks:
+    the fixed-point transport is an assignment problem, solved independently by
+    scipy's linear_sum_assignment; the simplex must reach the same optimum, fast."""
+    from scipy.optimize import linear_sum_assignment
+    rng = np.random.RandomState(7)
+    H = W = 64
+    cells = rng.choice(H * W, size=2000, replace=False)
+    a, b = np.zeros((H, W)), np.zeros((H, W))
+    a.flat[cells[:1000]] = 1.0
+    b.flat[cells[1000:]] = 1.0
+    t0 = time.perf_counter()
+    got = earth_mover_distance(a, b)
+    el = time.perf_counter() - t0
+    ys, xs = np.nonzero(a != b)
+    src = a[ys, xs] > 0
+    t = ground_distance_table(H, W)
+    C = t[ys[:, None] - ys[None, :] + H - 1, xs[:, None] - xs[None, :] + W - 1]
+    ic = np.floor(C * (1e6 / C.max()) + 0.5)[np.ix_(src, ~src)]
+    r, c = linear_sum_assignment(ic)
+    ref = ic[r, c].sum() * 1000 / (1e6 / 1000) / (1e6 / C.max())
+    assert abs(got - ref) <= 1e-9 * ref, (got, ref)
+    assert el < 60, el
+
+
+def test_side_effect_score_scaling():
+    """Scaling both densities scales the distance (masses are normalised by their
+    larger sum before rounding)."""
+    rng = np.random.RandomState(3)
+    a = rng.rand(26, 26) * (rng.rand(26, 26) < 0.2)
+    b = rng.rand(26, 26) * (rng.rand(26, 26) < 0.2)
+    e1 = earth_mover_distance(a, b)
+    e2 = earth_mover_distance(2 * a, 2 * b)
+    assert abs(e2 - 2 * e1) <= 1e-9 * e2
+    assert earth_mover_distance(a, a) == 0.0
