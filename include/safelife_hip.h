@@ -239,6 +239,23 @@ typedef struct sl_level_pool {
  * (safelife_game.py:184-194). */
 int sl_level_pool_prepare(sl_level_pool *pool, void *stream);
 
+/*
+ * Trajectory capture (SafeLifeRecorder, /root/reference/safelife/env_wrappers.py:97-136):
+ * sl_env_step copies the state of n chosen envs twice per step -- right after the
+ * board advance, before any reset (the frame the reference captures after
+ * env.step), and after the step's resets (the first frame of the next episode,
+ * meaningful where flags & 4).  Copies only; the stepping itself is unchanged.
+ */
+typedef struct sl_capture {
+    int32_t n;                    /* envs recorded (0: none)                       */
+    const int32_t *env;           /* dev [n] env indices                           */
+    uint16_t *board, *goals;      /* dev [n, H, W]  after the advance              */
+    int32_t *orientation;         /* dev [n]                                        */
+    uint8_t *flags;               /* dev [n]  the step's info flags                */
+    uint16_t *reset_board, *reset_goals;   /* dev [n, H, W]  after the resets     */
+    int32_t *reset_orientation;   /* dev [n]                                        */
+} sl_capture;
+
 typedef struct sl_env_cfg {
     int32_t time_limit;             /* SafeLifeEnv.time_limit (1000)          */
     int32_t auto_reset;             /* 1: ContinuingEnv + caller reset-on-done */
@@ -281,6 +298,8 @@ typedef struct sl_env_cfg {
                                        the board it holds on chip (no re-read) */
     int32_t obs_mode, obs_vh, obs_vw, obs_remove_white, obs_nch;
     int32_t obs_channels[16];
+    const sl_capture *capture;      /* host pointer or NULL: trajectory capture
+                                       (needs auto_reset and info_flags)      */
 } sl_env_cfg;
 
 /*

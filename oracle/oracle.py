@@ -544,6 +544,10 @@ class OracleEnv:
         self.last_side_effect = side
         info["side_effect"] = side
         done = bool(self.episode_completed)
+        # the state SafeLifeRecorder.capture_frame sees after env.step, before any reset
+        # (env_wrappers.py:118-126)
+        self.last_frame = (self.orientation, self.board.copy(), self.goals.copy(),
+                           bool(self.game_over))
         # ContinuingEnv + caller's reset-on-done
         if done and not times_up:
             done = False

@@ -681,6 +681,10 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);
+    if (fx.capture) {          // the frame before this step's resets
+        const int rc = launch_capture(st, *fx.capture, flags, 0, s);
+        if (rc) return rc;
+    }
     if (fx.fuse_reset && fx.pool.K > 0) {
         const unsigned grid = (unsigned)(st.B < 512 ? st.B : 512);
         sl::obs::ObsArgs oa{};

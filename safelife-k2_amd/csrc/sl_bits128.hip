@@ -383,6 +383,10 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
     hipLaunchKernelGGL(k_env_step_bits128, dim3((unsigned)st.B), dim3(64), 0, s, ka);
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);
+    if (fx.capture) {          // the frame before this step's resets
+        const int rc = launch_capture(st, *fx.capture, flags, 0, s);
+        if (rc) return rc;
+    }
     if (fx.fuse_reset && fx.pool.K > 0)
         return launch_reset_list_wide(st, fx.pool, fx.ra, fx.scratch, a.step, s);
     return SL_OK;

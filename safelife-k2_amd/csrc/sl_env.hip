@@ -920,6 +920,15 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     fx.ra = reset_args(cfg);
     fx.scratch = cfg->scratch;
     fx.ev_end = cfg->ev_end;
+    const sl_capture *cap = (cfg->capture && cfg->capture->n > 0) ? cfg->capture : nullptr;
+    if (cap && (!cap->env || !cap->board || !cap->goals || !cap->orientation || !cap->flags ||
+                !cap->reset_board || !cap->reset_goals || !cap->reset_orientation ||
+                !info_flags || !cfg->auto_reset))
+        return SL_EINVAL;
+    fx.capture = cap;
+    // the small-board kernel resets finished envs inside the step; with a capture the
+    // resets run in the follow-up scan so the pre-reset frame can be copied first
+    if (cap) fx.fuse_reset = 0;
     // observations: packed views of 64x64 boards come out of the step kernel itself
     ObsArgs oa;
     if (cfg->obs_out) {
@@ -985,17 +994,55 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     // step kernel and their reset-list kernel
     if (cfg->ev_end && !fast && !fast128) (void)hipEventRecord((hipEvent_t)cfg->ev_end, s);
 
+    if (cap && !fast && !fast128) {
+        const int rc = launch_capture(*st, *cap, info_flags, 0, s);
+        if (rc) return rc;
+    }
     if (cfg->auto_reset && !reset_done) {
         hipLaunchKernelGGL(k_env_reset_scan, dim3((unsigned)((B + NT - 1) / NT)), dim3(NT), 0, s,
                            *st, *pool, (const uint8_t *)info_flags, reset_args(cfg));
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
     }
     if (cfg->obs_out) {
-        if (!fuse_obs || (cfg->auto_reset && !reset_done))
-            return launch_obs(*st, oa, cfg->obs_out, s);
+        if (!fuse_obs || (cfg->auto_reset && !reset_done)) {
+            const int rc = launch_obs(*st, oa, cfg->obs_out, s);
+            if (rc) return rc;
+        }
         // else: the reset-list kernel wrote the views of the envs it reset
     }
+    if (cap) return launch_capture(*st, *cap, info_flags, 1, s);
     return SL_OK;
+}
+
+// ---------------------------------------------------------------------------
+// trajectory capture (sl_capture): one block per captured env, 16-byte copies
+// ---------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(NT)
+k_capture(sl_env_state st, sl_capture c, const uint8_t *__restrict__ flags, int phase) {
+    const int i = blockIdx.x;
+    const int64_t b = c.env[i];
+    if (b < 0 || b >= st.B) return;
+    const int64_t hw = (int64_t)st.H * st.W;
+    uint16_t *ob = (phase ? c.reset_board : c.board) + i * hw;
+    uint16_t *og = (phase ? c.reset_goals : c.goals) + i * hw;
+    const uint16_t *sb = st.board + b * hw, *sg = st.goals + b * hw;
+    for (int64_t k = threadIdx.x; k < hw; k += NT) {
+        ob[k] = sb[k];
+        og[k] = sg[k];
+    }
+    if (threadIdx.x == 0) {
+        (phase ? c.reset_orientation : c.orientation)[i] = st.orientation[b];
+        if (!phase) c.flags[i] = flags[b];
+    }
+}
+
+}  // namespace
+
+int sl::launch_capture(const sl_env_state &st, const sl_capture &c, const uint8_t *flags,
+                       int phase, hipStream_t s) {
+    hipLaunchKernelGGL(k_capture, dim3((unsigned)c.n), dim3(NT), 0, s, st, c, flags, phase);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
 extern "C" int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_white_goals,

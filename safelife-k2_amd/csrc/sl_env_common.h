@@ -245,7 +245,13 @@ struct FastExtra {
                             // (before any follow-up kernel), or NULL
     uint16_t *obs_out;      // 64x64 kernel: packed views written from the on-chip
     int32_t obs_vh, obs_vw, obs_rw;   // board (NULL: none); view shape, remove_white
+    const sl_capture *capture;        // trajectory capture (NULL: none): phase 0 is
+                                      // launched between the step and reset kernels
 };
+// copies of the captured envs' state (sl_capture): phase 0 after the advance (and
+// the step's flags), phase 1 after the resets
+int launch_capture(const sl_env_state &st, const sl_capture &c, const uint8_t *flags, int phase,
+                   hipStream_t s);
 // bit-sliced 128x128 kernel (sl_bits128.hip); needs the goals mirror (st.planes).
 // With fx.fuse_reset it queues the envs that finished and launches
 // k_env_reset_list_wide for them.

@@ -62,7 +62,14 @@ class EnvCfg(ctypes.Structure):
                 ("level_mode", i32), ("n_total_envs", i32), ("augment_roll", i32),
                 ("ev_begin", vp), ("ev_end", vp), ("kernel", i32),
                 ("obs_out", vp), ("obs_mode", i32), ("obs_vh", i32), ("obs_vw", i32),
-                ("obs_remove_white", i32), ("obs_nch", i32), ("obs_channels", i32 * 16)]
+                ("obs_remove_white", i32), ("obs_nch", i32), ("obs_channels", i32 * 16),
+                ("capture", vp)]
+
+
+class Capture(ctypes.Structure):
+    _fields_ = [("n", i32), ("env", vp), ("board", vp), ("goals", vp), ("orientation", vp),
+                ("flags", vp), ("reset_board", vp), ("reset_goals", vp),
+                ("reset_orientation", vp)]
 
 
 _lib = None

@@ -96,19 +96,27 @@ class LevelPool:
                          self.spawn_prob[idx], self.min_performance[idx])
 
     # -- device ---------------------------------------------------------------
-    def to_device(self, device):
+    def to_device(self, device, pin=False, non_blocking=False):
+        """Upload on the current stream (``pin``: through page-locked host buffers,
+        so ``non_blocking`` copies do not wait for the host)."""
         import torch
         if self._dev is not None and self._dev["device"] == device:
             return self._dev
+
+        def up(a):
+            h = torch.from_numpy(np.ascontiguousarray(a))
+            if pin:
+                h = h.pin_memory()
+            return h.to(device, non_blocking=non_blocking)
         t = {
             "device": device,
-            "board": torch.from_numpy(self.board).to(device),
-            "goals": torch.from_numpy(self.goals).to(device),
-            "agent_x": torch.from_numpy(self.agent_x).to(device),
-            "agent_y": torch.from_numpy(self.agent_y).to(device),
-            "orientation": torch.from_numpy(self.orientation).to(device),
-            "spawn_prob": torch.from_numpy(self.spawn_prob.astype(np.float32)).to(device),
-            "min_performance": torch.from_numpy(self.min_performance).to(device),
+            "board": up(self.board),
+            "goals": up(self.goals),
+            "agent_x": up(self.agent_x),
+            "agent_y": up(self.agent_y),
+            "orientation": up(self.orientation),
+            "spawn_prob": up(self.spawn_prob.astype(np.float32)),
+            "min_performance": up(self.min_performance),
         }
         s = _lib.LevelPool()
         s.K, s.H, s.W = self.K, self.H, self.W

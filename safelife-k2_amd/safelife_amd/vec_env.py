@@ -101,6 +101,7 @@ class SafeLifeVecEnv:
         self._last_step = None
         self._abandoned = 0          # explicit resets of episodes that had not ended
         self._synced = (0, 0)        # (started, completed) already in global_counter
+        self._recorder = None        # TrajectoryRecorder attached to this env
         self._alloc(obs_dtype)
         if rng == "stream":
             if spawn_stream is None:
@@ -259,6 +260,8 @@ class SafeLifeVecEnv:
                                   _lib.ptr(m), ctypes.byref(cfg), _lib.stream_ptr(self.device)),
                    "sl_env_reset")
         self.sync_counters()
+        if self._recorder is not None:
+            self._recorder.on_reset(None if m is None else m.cpu().numpy())
         return self.observe() if self.compute_obs else None
 
     def _running_mask(self):
@@ -326,6 +329,7 @@ class SafeLifeVecEnv:
         L = _lib.lib()
         cfg = self._fill_cfg()
         self._check_reset_lists()
+        cfg.capture = self._recorder._next_capture() if self._recorder is not None else None
         # the observation is written by sl_env_step itself (from the on-chip board
         # where the kernel allows it)
         obs = None

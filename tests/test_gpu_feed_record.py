@@ -1,0 +1,153 @@
+"""§8(f) rows 3 and 4 on the GPU: the asynchronous level-pool feeder and trajectory
+recording from device tensors, each against a synchronous / oracle restatement."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+POOLS = os.path.join(GOLDEN, "pools")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    import safelife_amd  # noqa: F401
+    return torch, torch.device("cuda:0")
+
+
+# ------------------------------------------------------------------ pool feeder
+@pytest.mark.parametrize("pool_name", ["c3_prune_still_64", "c2_append_still_25"])
+def test_pool_feeder_swap_matches_set_pool(torch_dev, pool_name):
+    """Levels produced on a host thread, uploaded on a side stream and swapped in
+    between steps give exactly the run of a synchronous set_pool at the same step;
+    resets after the swap draw from the new levels."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    from safelife_amd.pool_feed import PoolFeeder, npz_level_source
+    path = os.path.join(POOLS, pool_name + ".npz")
+    full = LevelPool.load(path)
+    first, second = full.subset(range(0, 8)), full.subset(range(8, 24))
+    B, T, swap_at = 64, 90, 30
+    kw = dict(time_limit=20, view_shape=(9, 9), output_channels=None, penalty_coef=1.0,
+              min_performance=0.01, rng="philox", seed=4, kernel="auto")
+    a = SafeLifeVecEnv(first, B, dev, **kw)
+    b = SafeLifeVecEnv(first, B, dev, **kw)
+    a.reset()
+    b.reset()
+    src = (lv for lv in list(npz_level_source(path, repeat=False))[8:24])
+    feeder = PoolFeeder(src, pool_size=16, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    try:
+        for t in range(T):
+            if t == swap_at:
+                assert feeder.swap(a, block=True, timeout=60)
+                b.set_pool(second)
+            act = torch.randint(0, 9, (B,), dtype=torch.int32, device=dev, generator=g)
+            _, r1, d1, i1 = a.step(act)
+            _, r2, d2, _ = b.step(act)
+            assert torch.equal(r1, r2) and torch.equal(d1, d2), t
+            assert torch.equal(a.board, b.board) and torch.equal(a.goals, b.goals), t
+        assert feeder.swaps == 1
+        # every env reset after the swap started from a level of the new pool
+        li = a.st_t["level_index"].cpu().numpy()
+        sb = a.start_board.cpu().numpy()
+        late = (a.st_t["episode_length"].cpu().numpy() < T - swap_at - 1)
+        assert late.any()
+        for e in np.nonzero(late)[0]:
+            assert np.array_equal(sb[e], second.board[li[e]]), e
+    finally:
+        feeder.close()
+
+
+# ---------------------------------------------------------------------- recorder
+def _exit_next_to_agent(levels):
+    """the levels with an open exit (min_performance -1) right of the agent"""
+    out = []
+    for lv in levels:
+        b = lv.board.copy()
+        H, W = b.shape
+        ax, ay = lv.agent_loc
+        b[ay, (ax + 1) % W] = 272
+        out.append(oracle.Level(b, lv.goals, lv.agent_loc, 1, lv.spawn_prob, -1.0))
+    return out
+
+
+def _expected_recordings(levels, env_ids, B, T, acts, kw, freq):
+    """SafeLifeRecorder + RecordingSafeLifeWrapper semantics (env_wrappers.py:97-286)
+    on oracle envs: a frame at the episode's start and after every step that leaves
+    the game not over; the episode is written when it ends (or at close)."""
+    out = {}
+    for e in env_ids:
+        o = oracle.OracleEnv(oracle.pool_level_fn(levels, e, n_total=B), env_id=e,
+                             rng="philox", seed=6, **kw)
+        o.reset()
+        eps, cur = [], None
+        frame = lambda: (o.orientation, o.board.copy(), o.goals.copy())   # noqa: E731
+        if o.episodes % freq == 0:
+            cur = (o.episodes, [frame()])
+        for t in range(T):
+            n0 = o.episodes
+            o.step(int(acts[t, e]))
+            orient, bd, gl, over = o.last_frame
+            if cur is not None and not over:
+                cur[1].append((orient, bd, gl))
+            if o.episodes != n0:
+                if cur is not None:
+                    eps.append(cur)
+                cur = (o.episodes, [frame()]) if o.episodes % freq == 0 else None
+        if cur is not None:
+            eps.append(cur)
+        out[e] = eps
+    return out
+
+
+@pytest.mark.parametrize("pool_name,kernel", [("c2_append_still_25", "auto"),
+                                              ("c3_prune_still_64", "auto"),
+                                              ("c5_navigation_128", "auto"),
+                                              ("c2_append_still_25", "generic")])
+def test_trajectory_recorder_vs_oracle(torch_dev, tmp_path, pool_name, kernel):
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    from safelife_amd.recorder import TrajectoryRecorder
+    d = np.load(os.path.join(POOLS, pool_name + ".npz"))
+    levels = _exit_next_to_agent([oracle.Level(d["board"][k], d["goals"][k], d["agent_loc"][k],
+                                               d["orientation"][k], d["spawn_prob"][k],
+                                               d["min_performance"][k])
+                                  for k in range(min(6, d["board"].shape[0]))])
+    pool = LevelPool.from_levels([{"board": lv.board, "goals": lv.goals,
+                                   "agent_loc": lv.agent_loc, "orientation": lv.orientation,
+                                   "spawn_prob": lv.spawn_prob,
+                                   "min_performance": lv.min_performance} for lv in levels])
+    B, T, freq = 8, 70, 2
+    env_ids = [0, 3, 7]
+    kw = dict(time_limit=13, view_shape=(5, 5), output_channels=None, penalty_coef=1.0,
+              min_performance=-1.0)
+    venv = SafeLifeVecEnv(pool, B, dev, rng="philox", seed=6, kernel=kernel, **kw)
+    venv.reset()
+    rec = TrajectoryRecorder(venv, str(tmp_path / "ep-{env}-{episode_num}"), env_ids=env_ids,
+                             video_recording_freq=freq, ring=16)
+    rng = np.random.RandomState(2)
+    acts = rng.choice(9, size=(T, B), p=[.04, .06, .5, .06, .06, .07, .07, .07, .07]).astype(np.int32)
+    overs = 0
+    for t in range(T):
+        venv.step(torch.from_numpy(acts[t]).to(dev))
+        overs += int(((venv.flags & 2) != 0).sum().item())
+    files = rec.close()
+    assert overs > 0                         # game-over endings were exercised
+    exp = _expected_recordings(levels, env_ids, B, T, acts, kw, freq)
+    for e in env_ids:
+        mine = sorted(f for f in files if os.path.basename(f).startswith("ep-%d-" % e))
+        mine.sort(key=lambda f: int(os.path.basename(f)[:-4].split("-")[2]))
+        assert [int(os.path.basename(f)[:-4].split("-")[2]) for f in mine] == \
+            [n for n, _ in exp[e]], e
+        for f, (num, frames) in zip(mine, exp[e]):
+            z = np.load(f)
+            assert z["board"].shape[0] == len(frames), (e, num)
+            assert np.array_equal(z["orientation"], [fr[0] for fr in frames]), (e, num)
+            assert np.array_equal(z["board"], np.stack([fr[1] for fr in frames])), (e, num)
+            assert np.array_equal(z["goals"], np.stack([fr[2] for fr in frames])), (e, num)

@@ -1,0 +1,62 @@
+"""npz_level_source: the static-level half of the reference's safelife_loader
+(file_finder.py:78-201) -- files, globs, directories, stacked pools; repeat and
+shuffle.  Host only."""
+import os
+
+import numpy as np
+import pytest
+
+from safelife_amd.pool_feed import npz_level_source
+from safelife_amd.levels import LevelPool
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_single_files_glob_and_directory():
+    files = sorted(os.path.join(GOLDEN, "levels", f)
+                   for f in os.listdir(os.path.join(GOLDEN, "levels")))
+    once = list(npz_level_source(os.path.join(GOLDEN, "levels", "append-still-*.npz"),
+                                 repeat=False))
+    assert len(once) == len(files) == 4
+    for lv, f in zip(once, files):
+        with np.load(f) as d:
+            assert np.array_equal(lv["board"], d["board"])
+    assert len(list(npz_level_source(os.path.join(GOLDEN, "levels"), repeat=False))) == 4
+    # the extension may be omitted, as file_finder.find_files allows
+    assert len(list(npz_level_source(files[0][:-4], repeat=False))) == 1
+    with pytest.raises(FileNotFoundError):
+        list(npz_level_source(os.path.join(GOLDEN, "nope")))
+
+
+def test_stacked_pool_repeat_and_shuffle():
+    path = os.path.join(GOLDEN, "pools", "c2_append_still_25.npz")
+    K = np.load(path)["board"].shape[0]
+    three = list(npz_level_source(path, repeat=3))
+    assert len(three) == 3 * K
+    assert all(np.array_equal(a["board"], b["board"]) for a, b in zip(three[:K], three[K:2 * K]))
+    src = npz_level_source(path, repeat=True, shuffle=True, seed=5)
+    first = [next(src)["board"] for _ in range(2 * K)]
+    # every pass is a permutation of the pool, and the passes differ
+    ref = sorted(np.load(path)["board"].reshape(K, -1).tolist())
+    assert sorted(b.reshape(-1).tolist() for b in first[:K]) == ref
+    assert any(not np.array_equal(a, b) for a, b in zip(first[:K], first[K:]))
+    pool = LevelPool.from_levels(three[:K])
+    assert pool.K == K
+
+
+def test_levels_archive(tmp_path):
+    """a structured `levels` archive (the v1.0 benchmark format, file_finder.py:89-93)"""
+    path = os.path.join(GOLDEN, "pools", "c2_append_still_25.npz")
+    d = np.load(path)
+    K, H, W = d["board"].shape
+    dt = np.dtype([("name", "U8"), ("board", np.uint16, (H, W)), ("goals", np.uint16, (H, W)),
+                   ("agent_loc", np.int64, (2,)), ("orientation", np.int64),
+                   ("spawn_prob", np.float64), ("min_performance", np.float64)])
+    arr = np.zeros(3, dt)
+    for i in range(3):
+        arr[i] = ("l%d" % i, d["board"][i], d["goals"][i], d["agent_loc"][i],
+                  d["orientation"][i], d["spawn_prob"][i], d["min_performance"][i])
+    np.savez(tmp_path / "archive.npz", levels=arr)
+    lv = list(npz_level_source(str(tmp_path / "archive.npz"), repeat=False))
+    assert len(lv) == 3 and np.array_equal(lv[2]["goals"], d["goals"][2])
+    assert LevelPool.from_levels(lv).K == 3
