@@ -12,7 +12,8 @@
 //   g.horiz(w0, w1)  columns col0-1 / col0+2 of a per-word quantity;
 //   g.halo_spawn()   a spawner sits in a row just outside the wave's words;
 //   g.cell(y, w)     the cell's flat index (the Philox counter of its draw);
-//   g.draws(...)     the spawn draws of the eligible cells (lane_draws).
+//   g.spawn(...)     the spawns among the eligible cells (SPAWN_PHILOX / _STREAM /
+//                    _COUNT below).
 #pragma once
 #include "sl_action.h"
 
@@ -101,6 +102,17 @@ template <int CTRL>
 __device__ __forceinline__ u32 dpp(u32 v) {
     return (u32)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
 }
+
+// Row masks (bit y) of the 64-byte sectors to write when lanes 16k .. 16k+15 hold
+// consecutive dwords of a row (the 128x128 layout): a lane's changed rows ORed over
+// its 16-lane DPP row.  Whole sectors are written, so HBM sees no partial bursts.
+__device__ __forceinline__ u32 sector_rows(u32 m) {
+    m |= dpp<0xB1>(m);     // quad_perm [1,0,3,2]
+    m |= dpp<0x4E>(m);     // quad_perm [2,3,0,1]
+    m |= dpp<0x141>(m);    // row_half_mirror
+    m |= dpp<0x140>(m);    // row_mirror
+    return m;
+}
 __device__ __forceinline__ int wave_total(int x) {
     u32 v = (u32)x;
     v += dpp<0xB1>(v);
@@ -129,6 +141,21 @@ struct SpawnCtx {
     double thr;
 };
 
+// How a geometry draws the spawns of its eligible cells (Geo::spawn):
+//   SPAWN_PHILOX  Philox keyed by (cell, env, step, tensor): no ordering needed;
+//   SPAWN_STREAM  the reference's order (SL_RNG_STREAM): a tensor's eligible cells take
+//                 consecutive uniforms of a supplied stream, row-major (stream_draws);
+//   SPAWN_COUNT   no draws: only count the eligible cells (the replay prologue kernels
+//                 that size each tensor's slice of the stream).
+enum : int { SPAWN_PHILOX = 0, SPAWN_STREAM = 1, SPAWN_COUNT = 2 };
+
+// the supplied stream (StepArgs draws / n_draws) and the error word (scratch[8B])
+struct StreamSrc {
+    const double *draws;
+    int64_t n;
+    int64_t *err;
+};
+
 // Spawn draws of the eligible cells elig[w] (bit y of word w), one lane at a time:
 // sp[w] gets the cells whose uniform is below the threshold.  A wave takes as many
 // Philox evaluations as its busiest lane has eligible cells.
@@ -147,6 +174,90 @@ __device__ __forceinline__ void lane_draws(const Geo &g, const u32 elig[2], u32 
         sp[w] = s;
     }
 }
+template <class Geo>
+__device__ __forceinline__ void philox_spawn(const Geo &g, const u32 elig[2], u32 sp[2],
+                                             const SpawnCtx &sc, u32 tensor) {
+    if (sc.thr <= 0.0) {                         // u < p never holds
+    } else if (sc.thr >= 1.0) {                  // u < p always holds
+        sp[0] = elig[0];
+        sp[1] = elig[1];
+    } else {
+        lane_draws(g, elig, sp, sc, tensor);
+    }
+}
+
+// number of set bits of m in the lanes below this one
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+}
+
+// Reference-order draws (SL_RNG_STREAM; random.c:47-52 consumed by advance_board.c:
+// 109-113): the eligible cells of a tensor take the uniforms draws[pos], draws[pos+1],
+// ... in row-major order -- one per eligible cell whatever p is -- and spawn iff
+// u < (double)(float)p.  Row bit y of word w of a lane is cell (row, 2j + w); the
+// cells before it are those of the earlier rows, those of lower lanes holding the
+// same row, and for w = 1 the lane's own word 0.  Rows are visited four at a time:
+// per row one ballot per word gives the row's eligible lanes (v_mbcnt counts the lower
+// ones), then the four rows' loads are issued together.  SPLIT: even lanes hold rows
+// y and odd lanes rows 32 + y (the 64x64 layout); else every lane holds row y.
+// Returns the number of uniforms the words consumed (wave-uniform).
+template <bool SPLIT>
+__device__ __forceinline__ int stream_draws(const u32 elig[2], u32 sp[2], double thr,
+                                            const StreamSrc &src, int64_t pos, int lane) {
+    constexpr uint64_t even = 0x5555555555555555ull;
+    const bool odd = SPLIT && (lane & 1);
+    const uint64_t grp = SPLIT ? (odd ? ~even : even) : ~0ull;
+    const int own = __builtin_popcount(elig[0]) + __builtin_popcount(elig[1]);
+    sp[0] = 0u;
+    sp[1] = 0u;
+    if (thr <= 0.0 || thr >= 1.0) {              // the draws are consumed, never compared
+        if (thr >= 1.0) {
+            sp[0] = elig[0];
+            sp[1] = elig[1];
+        }
+        return wave_total(own);
+    }
+    const int first = SPLIT ? wave_total(odd ? 0 : own) : 0;     // cells in rows 0..31
+    const u32 rows = wave_or(elig[0] | elig[1]);
+    int pre_a = 0, pre_b = 0;       // eligible cells of the visited rows (even / odd lanes)
+#pragma unroll
+    for (int c = 0; c < 32; c += 4) {
+        if (((rows >> c) & 0xFu) == 0u) continue;
+        int64_t r[4][2];
+        bool e[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int y = c + k;
+            e[k][0] = (elig[0] >> y) & 1u;
+            e[k][1] = (elig[1] >> y) & 1u;
+            const uint64_t m0 = __ballot(e[k][0]), m1 = __ballot(e[k][1]);
+            const int64_t at = pos + (odd ? first + pre_b : pre_a) + lanes_below(m0 & grp) +
+                               lanes_below(m1 & grp);
+            r[k][0] = at;
+            r[k][1] = at + (e[k][0] ? 1 : 0);
+            if (SPLIT) {
+                pre_a += __builtin_popcountll(m0 & even) + __builtin_popcountll(m1 & even);
+                pre_b += __builtin_popcountll(m0 & ~even) + __builtin_popcountll(m1 & ~even);
+            } else {
+                pre_a += __builtin_popcountll(m0) + __builtin_popcountll(m1);
+            }
+        }
+        double u[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int w = 0; w < 2; w++)
+                u[k][w] = (e[k][w] && r[k][w] < src.n) ? src.draws[r[k][w]] : 1.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int w = 0; w < 2; w++) {
+                if (e[k][w] && r[k][w] >= src.n) atomicOr((unsigned long long *)src.err, 1ull);
+                if (e[k][w] && u[k][w] < thr) sp[w] |= 1u << (c + k);
+            }
+    }
+    return pre_a + pre_b;
+}
 
 // One CA step of the planes P (in place).  chg[w] = cells that changed.
 // Appendix A: alive x survives iff frozen | P | cnt in {3,4}; dead x unless frozen | I
@@ -159,8 +270,8 @@ __device__ __forceinline__ void lane_draws(const Geo &g, const u32 elig[2], u32 
 // horizontally (word 0 sees columns col0-1 .. col0+1; word 1 sees col0 .. col0+2),
 // one quantity at a time so only the reduced results stay live.
 template <class Geo>
-__device__ __forceinline__ void rule_planes(u32 P[32], u32 chg[2], const Geo &g,
-                                            const SpawnCtx &sc, u32 tensor) {
+__device__ __forceinline__ void rule_planes(u32 P[32], u32 chg[2], Geo &&g, const SpawnCtx &sc,
+                                            u32 tensor) {
     u32 eq3[2], eq34[2];
     {   // 9-cell alive count: 3-row sums s = s0 + 2 s1, then t0 + 2h over 3 columns
         u32 s0[2], s1[2];
@@ -251,13 +362,7 @@ __device__ __forceinline__ void rule_planes(u32 P[32], u32 chg[2], const Geo &g,
             colk[k][0] |= h.l0 | vsc[k][0] | vsc[k][1];
             colk[k][1] |= vsc[k][0] | vsc[k][1] | h.r1;
         }
-        if (sc.thr <= 0.0) {            // u < p never holds
-        } else if (sc.thr >= 1.0) {                         // u < p always holds
-            sp[0] = elig[0];
-            sp[1] = elig[1];
-        } else {
-            g.draws(elig, sp, sc, tensor);
-        }
+        g.spawn(elig, sp, sc, tensor);
     }
     __builtin_amdgcn_sched_barrier(0);
     // ---- new planes

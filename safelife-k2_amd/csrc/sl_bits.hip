@@ -39,7 +39,8 @@ using namespace sl::bits;
 namespace {
 
 constexpr int kMinWaves = 4;      // waves per SIMD the register budget is sized for
-constexpr int kMinWavesObs = 3;   // the same for the instantiation that writes views
+constexpr int kMinWavesObs = 3;   // the same for the instantiations that write views or
+                                  // replay the reference stream
 
 constexpr int N = 64;        // rows = columns = lanes
 
@@ -48,8 +49,12 @@ constexpr int N = 64;        // rows = columns = lanes
 // 2j + 2 word 0 of lane l + 2 (the 64-lane rotation wraps at W = 64); the rows
 // around a word come from the other half's word (lane l ^ 1), which also supplies
 // the wrap at H = 64.
+template <int MODE>
 struct Geo64 {
     int lane;
+    StreamSrc src;     // SPAWN_STREAM: the supplied uniforms; pos = this tensor's first
+    int64_t pos;
+    int count;         // SPAWN_COUNT: this lane's eligible cells
     template <class F>
     __device__ __forceinline__ V3 vert(const u32 *P, int w, F f) const {
         const u32 x = f(P, w);
@@ -62,10 +67,16 @@ struct Geo64 {
     __device__ __forceinline__ u32 cell(int y, int w) const {
         return (u32)((32 * (lane & 1) + y) * N + 2 * (lane >> 1) + w);
     }
-    // spawners are rare on these boards: per-lane draws, no LDS list
-    __device__ __forceinline__ void draws(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
-                                          u32 tensor) const {
-        lane_draws(*this, elig, sp, sc, tensor);
+    // spawners are rare on these boards: per-lane Philox draws, no LDS list
+    __device__ __forceinline__ void spawn(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
+                                          u32 tensor) {
+        if (MODE == SPAWN_PHILOX) {
+            philox_spawn(*this, elig, sp, sc, tensor);
+        } else if (MODE == SPAWN_STREAM) {
+            (void)stream_draws<true>(elig, sp, sc.thr, src, pos, lane);
+        } else {
+            count += __builtin_popcount(elig[0]) + __builtin_popcount(elig[1]);
+        }
     }
 };
 
@@ -151,6 +162,32 @@ struct LdsCells {
         return reinterpret_cast<lds_cu16 *>(buf)[row * 64 + pos * 8 + (col & 7)];
     }
 };
+
+// The action's cell edits (wave-uniform (flat index, value) pairs) written into the
+// planes on the lane holding each cell; returns the row pairs (bit y: rows y, y + 32)
+// holding an edit, whose stores are then forced.
+__device__ __forceinline__ u32 mux_edits(u32 P[32], int ne, const int eidx[4], const u32 eval[4],
+                                         int lane) {
+    u32 erow = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (k < ne) {
+            const int y = eidx[k] >> 6, x = eidx[k] & 63;
+            const int tl = 2 * (x >> 1) + (y >> 5);            // lane holding the cell
+            const u32 bit = 1u << (y & 31);
+            const u32 m0 = (lane == tl && !(x & 1)) ? bit : 0u;
+            const u32 m1 = (lane == tl && (x & 1)) ? bit : 0u;
+            erow |= bit;
+#pragma unroll
+            for (int p = 0; p < 16; p++) {
+                const u32 v = ((eval[k] >> p) & 1u) ? ~0u : 0u;
+                PL(P, p, 0) = mux(m0, v, PL(P, p, 0));
+                PL(P, p, 1) = mux(m1, v, PL(P, p, 1));
+            }
+        }
+    }
+    return erow;
+}
 
 // SafeLifeEnv.reset (safelife_env.py:188-198) of env b by one wave, right after the
 // step that finished the episode (ContinuingEnv + run_agents' reset-on-done).
@@ -401,8 +438,10 @@ __device__ __forceinline__ void issue_pre(const sl_env_state &st, const int32_t 
 }
 
 // One env-step of env b.  `pre` holds b's record and goal colour planes and b's board
-// is in flight into `buf` (issued by the caller).
-template <bool OBS>
+// is in flight into `buf` (issued by the caller).  MODE: SPAWN_PHILOX, or SPAWN_STREAM
+// (replay: k_stream_prologue64 has run the action and sized the draws; the step reads
+// act[b] and each tensor's first uniform from the scratch words).
+template <bool OBS, int MODE>
 __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs &a,
                                          const FastExtra &fx, int64_t b, int lane, lds_u32 *buf,
                                          const int32_t *__restrict__ actions, int ctp, int ctc,
@@ -436,6 +475,14 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     sc.step = a.step;
     sc.seed = a.seed;
     sc.thr = (double)__int_as_float(rec(V, R_SPAWN));
+    StreamSrc ssrc{a.draws, a.n_draws, nullptr};
+    int64_t pos_b = 0, pos_g = 0;
+    if (MODE == SPAWN_STREAM) {
+        const Scratch w = scratch_of(fx.scratch, st.B);
+        ssrc.err = w.err;
+        pos_b = w.offsets[2 * b];
+        pos_g = w.offsets[2 * b + 1];
+    }
 
     // ---- goals
     if ((pok & 6) != 6) {
@@ -448,7 +495,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
             transpose32(PG);
         }
         u32 cg[2];
-        rule_planes(PG, cg, Geo64{lane}, sc, 1u);
+        rule_planes(PG, cg, Geo64<MODE>{lane, ssrc, pos_g, 0}, sc, 1u);
         const u32 rg = wave_or(cg[0] | cg[1]);
         if (mg) {      // mirror: the words whose 32 cells changed (all of them if rebuilt)
             const bool all = !(pok & 2);
@@ -491,9 +538,12 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
                rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     int act_reward = 0;
-    if (lane == 0)
-        act_reward = act_core(env, rec(V, R_ACT), N, N, ctp, ctc, ov);
-    act_reward = __builtin_amdgcn_readfirstlane(act_reward);
+    if (MODE == SPAWN_STREAM) {        // the prologue ran the action (no edits left)
+        act_reward = (int)scratch_of(fx.scratch, st.B).act[b];
+    } else {
+        if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ctp, ctc, ov);
+        act_reward = __builtin_amdgcn_readfirstlane(act_reward);
+    }
     const int ne = __builtin_amdgcn_readfirstlane(ov.n);
     int eidx[4];
     u32 eval[4];
@@ -515,26 +565,9 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     if (roll < 0) dma_board(st.start_board + off, buf, lane);
     else pool_dma(fx.pool, rec(V, R_LI), buf, lane);
     transpose32(PB);
-    u32 erow = 0;                      // row pairs (y, y + 32) holding an edit
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        if (k < ne) {
-            const int y = eidx[k] >> 6, x = eidx[k] & 63;
-            const int tl = 2 * (x >> 1) + (y >> 5);            // lane holding the cell
-            const u32 bit = 1u << (y & 31);
-            const u32 m0 = (lane == tl && !(x & 1)) ? bit : 0u;
-            const u32 m1 = (lane == tl && (x & 1)) ? bit : 0u;
-            erow |= bit;
-#pragma unroll
-            for (int p = 0; p < 16; p++) {
-                const u32 v = ((eval[k] >> p) & 1u) ? ~0u : 0u;
-                PL(PB, p, 0) = mux(m0, v, PL(PB, p, 0));
-                PL(PB, p, 1) = mux(m1, v, PL(PB, p, 1));
-            }
-        }
-    }
+    const u32 erow = mux_edits(PB, ne, eidx, eval, lane);
     u32 cb[2];
-    rule_planes(PB, cb, Geo64{lane}, sc, 0u);
+    rule_planes(PB, cb, Geo64<MODE>{lane, ssrc, pos_b, 0}, sc, 0u);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- scores over the new board and goals
@@ -622,13 +655,13 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         // queue the env for the reset kernel (k_env_reset_list)
         int64_t *cnt = fx.scratch + 8 * st.B + 2 + (a.step & 1);
         const int i = (int)atomicAdd((unsigned long long *)cnt, 1ull);
-        reinterpret_cast<int32_t *>(fx.scratch + 2 * st.B)[i] = (int32_t)b;
+        reset_list(fx.scratch)[i] = (int32_t)b;
     }
 }
 
-// OBS: also write the packed observation (fx.obs_out)
-template <bool OBS>
-__global__ void __launch_bounds__(64, OBS ? kMinWavesObs : kMinWaves)
+// OBS: also write the packed observation (fx.obs_out); MODE: see step_env
+template <bool OBS, int MODE>
+__global__ void __launch_bounds__(64, (OBS || MODE == SPAWN_STREAM) ? kMinWavesObs : kMinWaves)
 k_env_step_bits64(StepKArgs ka) {
     const int64_t b = blockIdx.x;          // one wave per env
     const int lane = threadIdx.x;
@@ -637,8 +670,77 @@ k_env_step_bits64(StepKArgs ka) {
     Pre pre;
     issue_pre(ka.st, ka.actions, b, lane, pre);
     dma_board(ka.st.board + b * (int64_t)(N * N), buf, lane);
-    step_env<OBS>(ka.st, ka.a, ka.fx, b, lane, buf, ka.actions, ka.ctp, ka.ctc, ka.reward_out,
+    step_env<OBS, MODE>(ka.st, ka.a, ka.fx, b, lane, buf, ka.actions, ka.ctp, ka.ctc, ka.reward_out,
                   ka.done_out, ka.flags_out, ka.ep_len_out, ka.ep_rew_out, pre);
+}
+
+// Replay-mode prologue of env b (SL_RNG_STREAM), one wave: the action (state, its
+// cell edits into the board in HBM, its reward into scratch act[b]), then the eligible
+// cells -- the uniforms the step will draw -- of the acted-on board and of the goals
+// (scratch counts[2b], [2b+1]; k_scan_i64 turns them into each tensor's first
+// uniform).  The work of k_env_action + k_env_count (sl_env.hip) on the bit-sliced rule.
+__global__ void __launch_bounds__(64)
+k_stream_prologue64(StepKArgs ka) {
+    const sl_env_state &st = ka.st;
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t off = b * (int64_t)(N * N);
+    const int lane_off = (lane & 1) * 1024 + (lane >> 1);
+    const u32 V = load_record(st, ka.actions, b, lane);
+    u32 P[32];
+    load_pairs<32>(reinterpret_cast<const u32 *>(st.board + off) + lane_off, P);
+    OverlayT<GlobalCells> ov;
+    ov.src.bd = st.board + off;
+    ov.n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        ov.idx[k] = 0;
+        ov.val[k] = 0;
+    }
+    RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
+               rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
+    const Scratch w = scratch_of(ka.fx.scratch, st.B);
+    if (lane == 0) {
+        w.act[b] = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
+        // the edits: into HBM for the step kernel, into the planes below for the count
+        // (whether the wave's loads saw these stores does not matter)
+        for (int k = 0; k < ov.n; k++) st.board[off + ov.idx[k]] = (uint16_t)ov.val[k];
+    }
+    const int ne = __builtin_amdgcn_readfirstlane(ov.n);
+    int eidx[4];
+    u32 eval[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        eidx[k] = __builtin_amdgcn_readfirstlane(ov.idx[k]);
+        eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
+    }
+    SpawnCtx sc{0u, 0u, 0ull, 0.0};
+    transpose32(P);
+    (void)mux_edits(P, ne, eidx, eval, lane);
+    u32 ch[2];
+    Geo64<SPAWN_COUNT> gbd{lane, StreamSrc{nullptr, 0, nullptr}, 0, 0};
+    rule_planes(P, ch, gbd, sc, 0u);
+    const int nb = wave_total(gbd.count);
+    // goals at their fixed point (planes_ok bit 2) hold no spawner: no draws
+    const int pok = (st.planes && st.planes_ok) ? rec(V, R_POK) & 6 : 0;
+    int ng = 0;
+    if ((pok & 6) != 6) {
+        if (pok & 2) {
+            const u32 *mg = st.planes + b * 4096 + 2048 + lane;
+#pragma unroll
+            for (int q = 0; q < 32; q++) P[q] = mg[q * 64];
+        } else {
+            load_pairs<32>(reinterpret_cast<const u32 *>(st.goals + off) + lane_off, P);
+            transpose32(P);
+        }
+        Geo64<SPAWN_COUNT> ggl{lane, StreamSrc{nullptr, 0, nullptr}, 0, 0};
+        rule_planes(P, ch, ggl, sc, 1u);
+        ng = wave_total(ggl.count);
+    }
+    if (lane == 0) {
+        w.counts[2 * b] = nb;
+        w.counts[2 * b + 1] = ng;
+    }
 }
 
 // Resets the envs the step kernel queued (one wave per env, grid-stride over the
@@ -651,7 +753,7 @@ k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scr
     int64_t *cnt = scratch + 8 * st.B + 2;
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(step + 1) & 1] = 0;
     const int n = (int)__builtin_amdgcn_readfirstlane((int)cnt[step & 1]);
-    const int32_t *list = reinterpret_cast<const int32_t *>(scratch + 2 * st.B);
+    const int32_t *list = reset_list(scratch);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int64_t b = __builtin_amdgcn_readfirstlane(list[i]);
         wave_reset(st, pool, ra, b, threadIdx.x);
@@ -673,11 +775,24 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
     if (st.H != N || st.W != N) return SL_ETOOBIG;
     const unsigned grid = (unsigned)st.B;
     const StepKArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
-    if (fx.obs_out) {
-        if (fx.obs_vh < 1 || fx.obs_vw < 1 || fx.obs_vh * fx.obs_vw > 4096) return SL_EINVAL;
-        hipLaunchKernelGGL(k_env_step_bits64<true>, dim3(grid), dim3(64), 0, s, ka);
+    if (fx.obs_out && (fx.obs_vh < 1 || fx.obs_vw < 1 || fx.obs_vh * fx.obs_vw > 4096))
+        return SL_EINVAL;
+    if (fx.stream) {
+        hipLaunchKernelGGL(k_stream_prologue64, dim3(grid), dim3(64), 0, s, ka);
+        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        const int rc = stream_offsets(st, fx, s);
+        if (rc) return rc;
+        if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
+        if (fx.obs_out)
+            hipLaunchKernelGGL((k_env_step_bits64<true, SPAWN_STREAM>), dim3(grid), dim3(64), 0, s, ka);
+        else
+            hipLaunchKernelGGL((k_env_step_bits64<false, SPAWN_STREAM>), dim3(grid), dim3(64), 0, s, ka);
     } else {
-        hipLaunchKernelGGL(k_env_step_bits64<false>, dim3(grid), dim3(64), 0, s, ka);
+        if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
+        if (fx.obs_out)
+            hipLaunchKernelGGL((k_env_step_bits64<true, SPAWN_PHILOX>), dim3(grid), dim3(64), 0, s, ka);
+        else
+            hipLaunchKernelGGL((k_env_step_bits64<false, SPAWN_PHILOX>), dim3(grid), dim3(64), 0, s, ka);
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);

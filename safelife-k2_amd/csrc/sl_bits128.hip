@@ -17,7 +17,7 @@
 //    read before any band is written back, so every band sees the pre-step board;
 //  * points, performance score, possible score and side effects
 //    (safelife_game.py:590-631, env_wrappers.py:319-342) are summed band by band;
-//    only the rows that changed are stored;
+//    only the 64-byte row sectors that changed are stored (16 lanes' words);
 //  * goals: a bit-plane mirror (sl_env_state.planes, [B][band][32 words][64 lanes])
 //    holds their planes.  Goals without spawners that came through a step unchanged
 //    are at a fixed point of the rule (planes_ok bit 2): the rule is skipped and only
@@ -61,9 +61,14 @@ struct HaloView {
 // Neighbourhood of a band word: columns from the neighbouring lanes (2j - 1 is word
 // 1 of lane j - 1, 2j + 2 word 0 of lane j + 1), rows outside the band from the halo
 // (plane k, word w: bit 31 = row 32t - 1, bit 0 = row 32t + 32).
+template <int MODE>
 struct GeoBand {
     int lane, row0;
     HaloView hv;
+    StreamSrc src;     // SPAWN_STREAM: the supplied uniforms; pos = the band's first,
+    int64_t pos;       // used = how many the band consumed
+    int used;
+    int count;         // SPAWN_COUNT: this lane's eligible cells
     template <class F>
     __device__ __forceinline__ V3 vert(const u32 *P, int w, F f) const {
         return vert_with(f(P, w), f(hv, w));
@@ -78,9 +83,15 @@ struct GeoBand {
     __device__ __forceinline__ u32 cell_at(int l, int y, int w) const {
         return (u32)((row0 + y) * N + 2 * l + w);
     }
-    __device__ __forceinline__ void draws(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
-                                          u32 tensor) const {
-        lane_draws(*this, elig, sp, sc, tensor);
+    __device__ __forceinline__ void spawn(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
+                                          u32 tensor) {
+        if (MODE == SPAWN_PHILOX) {
+            philox_spawn(*this, elig, sp, sc, tensor);
+        } else if (MODE == SPAWN_STREAM) {
+            used = stream_draws<false>(elig, sp, sc.thr, src, pos, lane);
+        } else {
+            count += __builtin_popcount(elig[0]) + __builtin_popcount(elig[1]);
+        }
     }
 };
 
@@ -190,6 +201,10 @@ __device__ __forceinline__ const Step128KArgs &kargs128() {
     return *(const Step128KArgs *)kp;
 }
 
+// MODE: SPAWN_PHILOX, or SPAWN_STREAM (replay: k_stream_prologue128 has run the action
+// and sized the draws; the step reads act[b] and each tensor's first uniform from the
+// scratch words)
+template <int MODE>
 __global__ void __launch_bounds__(64, kMinWaves)
 k_env_step_bits128(Step128KArgs ka) {
     const sl_env_state &st = ka.st;
@@ -222,6 +237,14 @@ k_env_step_bits128(Step128KArgs ka) {
     sc.step = a.step;
     sc.seed = a.seed;
     sc.thr = (double)__int_as_float(rec(V, R_SPAWN));
+    StreamSrc ssrc{a.draws, a.n_draws, nullptr};
+    int64_t pos_b = 0, pos_g = 0;
+    if (MODE == SPAWN_STREAM) {
+        const Scratch w = scratch_of(fx.scratch, st.B);
+        ssrc.err = w.err;
+        pos_b = w.offsets[2 * b];
+        pos_g = w.offsets[2 * b + 1];
+    }
 
     // ---- goals: advanced band by band unless at a fixed point; the mirror keeps
     // their planes (all words rewritten when it was stale, else the changed ones)
@@ -240,8 +263,9 @@ k_env_step_bits128(Step128KArgs ka) {
             load_pairs<RS>(gg + 32 * t * RS, G);
             transpose32(G);
             u32 cg[2];
-            rule_planes(G, cg, GeoBand{lane, 32 * t, HaloView{pick4(gu, t), pick4(gd, t)}}, sc,
-                        1u);
+            GeoBand<MODE> geo{lane, 32 * t, HaloView{pick4(gu, t), pick4(gd, t)}, ssrc, pos_g, 0, 0};
+            rule_planes(G, cg, geo, sc, 1u);
+            pos_g += geo.used;
             const u32 rg = wave_or(cg[0] | cg[1]);
             u32 *m = mg + t * MW;       // only the colour planes are ever read back
 #pragma unroll
@@ -253,7 +277,11 @@ k_env_step_bits128(Step128KArgs ka) {
             spawners |= PL(G, 7, 0) | PL(G, 7, 1);
             if (rg) {
                 transpose32(G);
-                store_pairs<RS>(gg + 32 * t * RS, G, rg);
+                const u32 lm = sector_rows(cg[0] | cg[1]);
+#pragma unroll
+                for (int y = 0; y < 32; y++)
+                    if ((rg >> y) & 1u)
+                        if ((lm >> y) & 1u) gg[(32 * t + y) * RS] = G[y];
             }
         }
         const bool fixed = changed == 0 && __ballot(spawners != 0u) == 0ull;
@@ -275,8 +303,12 @@ k_env_step_bits128(Step128KArgs ka) {
     RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
                rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     int act_reward = 0;
-    if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ctp, ctc, ov);
-    act_reward = __builtin_amdgcn_readfirstlane(act_reward);
+    if (MODE == SPAWN_STREAM) {        // the prologue ran the action (no edits left)
+        act_reward = (int)scratch_of(fx.scratch, st.B).act[b];
+    } else {
+        if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ctp, ctc, ov);
+        act_reward = __builtin_amdgcn_readfirstlane(act_reward);
+    }
     const int ne = __builtin_amdgcn_readfirstlane(ov.n);
     int eidx[4];
     u32 eval[4];
@@ -315,18 +347,19 @@ k_env_step_bits128(Step128KArgs ka) {
     for (int t = 0; t < NB; t++) {
         u32 P[32], S[32];
         load_pairs<RS>(gb + 32 * t * RS, P);
-        if (roll < 0) {
-            load_pairs<RS>(gs + 32 * t * RS, S);      // in flight under the rule
-        } else {
+        if (roll >= 0) {
             wait_lgkm();        // the previous band's reads of the buffer are done
             pool_dma128(pp, t, sdy, lane, spool);
         }
         transpose32(P);
         const u32 erow = apply_edits(P, ne, eidx, eval, 32 * t, lane);
         u32 cb[2];
-        rule_planes(P, cb, GeoBand{lane, 32 * t, HaloView{pick4(bu, t), pick4(bd, t)}}, sc, 0u);
+        GeoBand<MODE> geo{lane, 32 * t, HaloView{pick4(bu, t), pick4(bd, t)}, ssrc, pos_b, 0, 0};
+        rule_planes(P, cb, geo, sc, 0u);
+        pos_b += geo.used;
         __builtin_amdgcn_sched_barrier(0);
         if (roll < 0) {
+            load_pairs<RS>(gs + 32 * t * RS, S);
             transpose32(S);
         } else {
             wait_vm();          // the band's pool planes have landed in LDS
@@ -348,7 +381,13 @@ k_env_step_bits128(Step128KArgs ka) {
         const u32 rb = wave_or(cb[0] | cb[1]) | erow;
         if (rb) {
             transpose32(P);
-            store_pairs<RS>(gb + 32 * t * RS, P, rb);
+            // only the changed 64-byte row sectors (inline: as a helper call the
+            // compiler gives this kernel 30 more VGPRs and drops it to 2 waves/SIMD)
+            const u32 lm = sector_rows(cb[0] | cb[1]) | erow;
+#pragma unroll
+            for (int y = 0; y < 32; y++)
+                if ((rb >> y) & 1u)
+                    if ((lm >> y) & 1u) gb[(32 * t + y) * RS] = P[y];
         }
     }
     const int points = wave_total(pts), score = wave_total(scr);
@@ -362,8 +401,80 @@ k_env_step_bits128(Step128KArgs ka) {
         if (k.fx.fuse_reset && reset) {   // queued for k_env_reset_list_wide
             int64_t *cnt = k.fx.scratch + 8 * k.st.B + 2 + (k.a.step & 1);
             const int i = (int)atomicAdd((unsigned long long *)cnt, 1ull);
-            reinterpret_cast<int32_t *>(k.fx.scratch + 2 * k.st.B)[i] = (int32_t)b;
+            reset_list(k.fx.scratch)[i] = (int32_t)b;
         }
+    }
+}
+
+// Replay-mode prologue of env b (SL_RNG_STREAM), one wave: the action (state, its
+// cell edits into the board in HBM, its reward into scratch act[b]), then the eligible
+// cells of the acted-on board and of the goals, band by band (scratch counts[2b],
+// [2b+1]; k_scan_i64 turns them into each tensor's first uniform).  The work of
+// k_env_action + k_env_count (sl_env.hip) on the bit-sliced rule.
+__global__ void __launch_bounds__(64)
+k_stream_prologue128(Step128KArgs ka) {
+    const sl_env_state &st = ka.st;
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t off = b * (int64_t)(N * N);
+    const u32 *gb = reinterpret_cast<const u32 *>(st.board + off) + lane;
+    const u32 *gg = reinterpret_cast<const u32 *>(st.goals + off) + lane;
+    const u32 V = load_record(st, ka.actions, b, lane);
+    OverlayT<GlobalCells> ov;
+    ov.src.bd = st.board + off;
+    ov.n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        ov.idx[k] = 0;
+        ov.val[k] = 0;
+    }
+    RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
+               rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
+    const Scratch w = scratch_of(ka.fx.scratch, st.B);
+    if (lane == 0) {
+        w.act[b] = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
+        // into HBM for the step kernel; into the planes and halo rows below for the
+        // count (whether this wave's loads see these stores does not matter)
+        for (int k = 0; k < ov.n; k++) st.board[off + ov.idx[k]] = (uint16_t)ov.val[k];
+    }
+    const int ne = __builtin_amdgcn_readfirstlane(ov.n);
+    int eidx[4];
+    u32 eval[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        eidx[k] = __builtin_amdgcn_readfirstlane(ov.idx[k]);
+        eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
+    }
+    SpawnCtx sc{0u, 0u, 0ull, 0.0};
+    const StreamSrc none{nullptr, 0, nullptr};
+    // the eligible cells of one tensor (edited: the board), band by band
+    auto count = [&](const u32 *g, bool edited) {
+        int n = 0;
+#pragma unroll 1
+        for (int t = 0; t < NB; t++) {
+            const int ru = (32 * t - 1) & (N - 1), rd = (32 * t + 32) & (N - 1);
+            u32 up = g[ru * RS], dn = g[rd * RS];
+            u32 P[32];
+            load_pairs<RS>(g + 32 * t * RS, P);
+            transpose32(P);
+            if (edited && ne > 0) {
+                up = edit_row(up, ru, ne, eidx, eval, lane);
+                dn = edit_row(dn, rd, ne, eidx, eval, lane);
+                (void)apply_edits(P, ne, eidx, eval, 32 * t, lane);
+            }
+            GeoBand<SPAWN_COUNT> geo{lane, 32 * t, HaloView{up, dn}, none, 0, 0, 0};
+            u32 ch[2];
+            rule_planes(P, ch, geo, sc, 0u);
+            n += geo.count;
+        }
+        return wave_total(n);
+    };
+    const int nb = count(gb, true);
+    // goals at their fixed point (planes_ok bit 2) hold no spawner: no draws
+    const int ng = (rec(V, R_POK) & 6) == 6 ? 0 : count(gg, false);
+    if (lane == 0) {
+        w.counts[2 * b] = nb;
+        w.counts[2 * b + 1] = ng;
     }
 }
 
@@ -380,7 +491,18 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
                         uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (!bits128_shape(st)) return SL_ETOOBIG;
     const Step128KArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
-    hipLaunchKernelGGL(k_env_step_bits128, dim3((unsigned)st.B), dim3(64), 0, s, ka);
+    const dim3 grid((unsigned)st.B);
+    if (fx.stream) {
+        hipLaunchKernelGGL(k_stream_prologue128, grid, dim3(64), 0, s, ka);
+        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        const int rc = stream_offsets(st, fx, s);
+        if (rc) return rc;
+        if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
+        hipLaunchKernelGGL(k_env_step_bits128<SPAWN_STREAM>, grid, dim3(64), 0, s, ka);
+    } else {
+        if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
+        hipLaunchKernelGGL(k_env_step_bits128<SPAWN_PHILOX>, grid, dim3(64), 0, s, ka);
+    }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);
     if (fx.capture) {          // the frame before this step's resets

@@ -20,7 +20,9 @@
 //  * points, performance score, possible score and side effects
 //    (safelife_game.py:590-631, env_wrappers.py:319-342) are recomputed in full from
 //    the planes; only changed rows are stored; the epilogue is the shared one.
-// Resets after the step are done by k_env_reset_scan (sl_env.hip).  Philox mode only.
+// Finished envs are reset by their own wave at the end of the step (small_reset).
+// Philox draws, or the reference's stream order after a replay prologue
+// (k_stream_prologue_small).
 #include "sl_bits.h"
 
 using namespace sl;
@@ -31,11 +33,15 @@ namespace {
 
 constexpr int kMaxH = 32, kMaxW = 64;
 
+template <int MODE>
 struct GeoSmall {
     int lane, H, W, nl;
     u32 mh;                  // the low H bits
     int src_l, src_r;        // lanes holding columns 2j - 1 and 2j + 2
     bool odd_last;           // this lane's word 1 is the column-0 copy (odd W)
+    StreamSrc src;           // SPAWN_STREAM: the supplied uniforms from this tensor's first
+    int64_t pos;
+    int count;               // SPAWN_COUNT: this lane's eligible cells
     template <class F>
     __device__ __forceinline__ V3 vert(const u32 *P, int w, F f) const {
         const u32 x = f(P, w);
@@ -48,11 +54,40 @@ struct GeoSmall {
     }
     __device__ __forceinline__ bool halo_spawn() const { return false; }
     __device__ __forceinline__ u32 cell(int y, int w) const { return (u32)(y * W + 2 * lane + w); }
-    __device__ __forceinline__ void draws(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
-                                          u32 tensor) const {
-        lane_draws(*this, elig, sp, sc, tensor);
+    // (the column-0 copy's draws are discarded with the rest of that word; in replay
+    // mode it draws nothing, so it cannot shift the real cells' ranks)
+    __device__ __forceinline__ void spawn(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
+                                          u32 tensor) {
+        const u32 e[2] = {elig[0], odd_last ? 0u : elig[1]};
+        if (MODE == SPAWN_PHILOX) {
+            philox_spawn(*this, elig, sp, sc, tensor);
+        } else if (MODE == SPAWN_STREAM) {
+            (void)stream_draws<false>(e, sp, sc.thr, src, pos, lane);
+        } else {
+            count += __builtin_popcount(e[0]) + __builtin_popcount(e[1]);
+        }
     }
 };
+
+// the geometry of lane `lane` on an H x W board (lanes >= ceil(W / 2) hold nothing)
+template <int MODE>
+__device__ __forceinline__ GeoSmall<MODE> small_geo(int lane, int H, int W) {
+    GeoSmall<MODE> g;
+    const int nl = (W + 1) >> 1;
+    const bool active = lane < nl;
+    g.lane = lane;
+    g.H = H;
+    g.W = W;
+    g.nl = nl;
+    g.mh = H == 32 ? ~0u : ((1u << H) - 1u);
+    g.src_l = active ? (lane == 0 ? nl - 1 : lane - 1) : lane;
+    g.src_r = active ? (lane + 1 == nl ? 0 : lane + 1) : lane;
+    g.odd_last = (W & 1) && lane == nl - 1;
+    g.src = StreamSrc{nullptr, 0, nullptr};
+    g.pos = 0;
+    g.count = 0;
+    return g;
+}
 
 typedef __attribute__((address_space(3))) u32 lds_u32;
 typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
@@ -134,6 +169,7 @@ struct SmallKArgs {
     int32_t *ep_len_out, *ep_rew_out;
     sl_level_pool pool;       // auto-reset source (K == 0: no reset here)
     ResetArgs ra;
+    int64_t *scratch;         // sl_env_cfg.scratch (replay mode: act, offsets, err)
 };
 
 __device__ __forceinline__ const SmallKArgs &kargs() {
@@ -229,6 +265,10 @@ __device__ __forceinline__ void small_reset(const sl_env_state &st, const sl_lev
     }
 }
 
+// MODE: SPAWN_PHILOX, or SPAWN_STREAM (replay: k_stream_prologue_small has run the
+// action and sized the draws; the step reads act[b] and each tensor's first uniform
+// from the scratch words)
+template <int MODE>
 __global__ void __launch_bounds__(64, SL_SMALL_MINW)
 k_env_step_small(SmallKArgs ka) {
     const sl_env_state &st = ka.st;
@@ -245,15 +285,14 @@ k_env_step_small(SmallKArgs ka) {
     lds_u32 *buf = (lds_u32 *)stage[0];
     const bool active = lane < nl;
     const int c0 = 2 * lane, c1 = 2 * lane + 1;             // stores: c1 < W unless odd_last
-    GeoSmall geo;
-    geo.lane = lane;
-    geo.H = H;
-    geo.W = W;
-    geo.nl = nl;
-    geo.mh = H == 32 ? ~0u : ((1u << H) - 1u);
-    geo.src_l = active ? (lane == 0 ? nl - 1 : lane - 1) : lane;
-    geo.src_r = active ? (lane + 1 == nl ? 0 : lane + 1) : lane;
-    geo.odd_last = (W & 1) && lane == nl - 1;
+    GeoSmall<MODE> geo = small_geo<MODE>(lane, H, W);
+    int64_t pos_b = 0, pos_g = 0;
+    if (MODE == SPAWN_STREAM) {
+        const Scratch w = scratch_of(ka.scratch, st.B);
+        geo.src = StreamSrc{a.draws, a.n_draws, w.err};
+        pos_b = w.offsets[2 * b];
+        pos_g = w.offsets[2 * b + 1];
+    }
     // valid cells per word: rows < H of real columns
     const u32 wm0 = active ? geo.mh : 0u, wm1 = (active && !geo.odd_last) ? geo.mh : 0u;
 
@@ -278,6 +317,7 @@ k_env_step_small(SmallKArgs ka) {
     // ---- goals: rule, then store the changed rows
     transpose32(PG);
     u32 cg[2];
+    geo.pos = pos_g;
     rule_planes(PG, cg, geo, sc, 1u);
     cg[0] &= wm0;
     cg[1] &= wm1;
@@ -312,8 +352,12 @@ k_env_step_small(SmallKArgs ka) {
     RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
                rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     int act_reward = 0;
-    if (lane == 0) act_reward = act_core<64>(env, rec(V, R_ACT), H, W, ctp, ctc, ov);
-    act_reward = __builtin_amdgcn_readfirstlane(act_reward);
+    if (MODE == SPAWN_STREAM) {        // the prologue ran the action (no edits left)
+        act_reward = (int)scratch_of(ka.scratch, st.B).act[b];
+    } else {
+        if (lane == 0) act_reward = act_core<64>(env, rec(V, R_ACT), H, W, ctp, ctc, ov);
+        act_reward = __builtin_amdgcn_readfirstlane(act_reward);
+    }
     // the action's cell edits go straight into the staged board (lane 0; the wave's LDS
     // operations run in order, so the row reads below see them), the column-0 copy of
     // an odd board too; erow = the rows holding an edit
@@ -339,6 +383,7 @@ k_env_step_small(SmallKArgs ka) {
     lds_rows((const lds_u16 *)stage[0], H, active, lane, PB);
     transpose32(PB);
     u32 cb[2];
+    geo.pos = pos_b;
     rule_planes(PB, cb, geo, sc, 0u);
     __builtin_amdgcn_sched_barrier(0);
 
@@ -396,6 +441,67 @@ k_env_step_small(SmallKArgs ka) {
     }
 }
 
+// Replay-mode prologue of env b (SL_RNG_STREAM), one wave: the action (state, its
+// cell edits into the board in HBM, its reward into scratch act[b]), then the eligible
+// cells of the acted-on board and of the goals (scratch counts[2b], [2b+1];
+// k_scan_i64 turns them into each tensor's first uniform).  The work of k_env_action
+// + k_env_count (sl_env.hip) on the bit-sliced rule.
+__global__ void __launch_bounds__(64)
+k_stream_prologue_small(SmallKArgs ka) {
+    const sl_env_state &st = ka.st;
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int H = st.H, W = st.W, nl = (W + 1) >> 1;
+    extern __shared__ __attribute__((aligned(16))) u32 dyn_stage[];
+    u32 *stage[3] = {dyn_stage, dyn_stage + H * 32, dyn_stage + 2 * H * 32};
+    const bool active = lane < nl;
+    const int64_t off = b * (int64_t)H * W;
+    const u32 V = load_record(st, ka.actions, b, lane);
+    {
+        const uint16_t *src[3] = {st.board + off, st.goals + off, st.start_board + off};
+        lds_u16 *dst[3] = {(lds_u16 *)stage[0], (lds_u16 *)stage[1], (lds_u16 *)stage[2]};
+        stage_tensors(src, dst, H * W, W, lane);
+    }
+    wait_lgkm();
+    OverlayT<SmallCells> ov;
+    ov.src.buf = (lds_u32 *)stage[0];
+    ov.n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        ov.idx[k] = 0;
+        ov.val[k] = 0;
+    }
+    RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
+               rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
+    const Scratch w = scratch_of(ka.scratch, st.B);
+    if (lane == 0) {
+        w.act[b] = act_core<64>(env, rec(V, R_ACT), H, W, ka.ctp, ka.ctc, ov);
+        lds_u16 *cells = (lds_u16 *)stage[0];
+        for (int k = 0; k < ov.n; k++) {
+            const int i = ov.idx[k], y = i >> 6, x = i & 63;
+            cells[i] = (uint16_t)ov.val[k];
+            if ((W & 1) && x == 0) cells[i + W] = (uint16_t)ov.val[k];
+            st.board[off + y * W + x] = (uint16_t)ov.val[k];
+        }
+    }
+    SpawnCtx sc{0u, 0u, 0ull, 0.0};
+    int n[2];
+#pragma unroll 1
+    for (int t = 0; t < 2; t++) {
+        u32 P[32];
+        lds_rows((const lds_u16 *)stage[t], H, active, lane, P);
+        transpose32(P);
+        GeoSmall<SPAWN_COUNT> geo = small_geo<SPAWN_COUNT>(lane, H, W);
+        u32 ch[2];
+        rule_planes(P, ch, geo, sc, (u32)t);
+        n[t] = wave_total(geo.count);
+    }
+    if (lane == 0) {
+        w.counts[2 * b] = n[0];
+        w.counts[2 * b + 1] = n[1];
+    }
+}
+
 }  // namespace
 
 namespace sl {
@@ -412,9 +518,20 @@ int launch_step_small(const sl_env_state &st, const StepArgs &a, const FastExtra
     sl_level_pool pool = fx.pool;
     if (!fx.fuse_reset || pool.H != st.H || pool.W != st.W) pool.K = 0;
     const SmallKArgs ka{st, a, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew, pool,
-                        fx.ra};
+                        fx.ra, fx.scratch};
     const size_t lds = (size_t)3 * st.H * 32 * sizeof(uint32_t);
-    hipLaunchKernelGGL(k_env_step_small, dim3((unsigned)st.B), dim3(64), lds, s, ka);
+    const dim3 grid((unsigned)st.B);
+    if (fx.stream) {
+        hipLaunchKernelGGL(k_stream_prologue_small, grid, dim3(64), lds, s, ka);
+        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        const int rc = stream_offsets(st, fx, s);
+        if (rc) return rc;
+        if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
+        hipLaunchKernelGGL(k_env_step_small<SPAWN_STREAM>, grid, dim3(64), lds, s, ka);
+    } else {
+        if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
+        hipLaunchKernelGGL(k_env_step_small<SPAWN_PHILOX>, grid, dim3(64), lds, s, ka);
+    }
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 

@@ -505,7 +505,7 @@ k_env_reset_list_wide(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t
     int64_t *cnt = scratch + 8 * st.B + 2;
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(step + 1) & 1] = 0;
     const int n = (int)cnt[step & 1];
-    const int32_t *list = reinterpret_cast<const int32_t *>(scratch + 2 * st.B);
+    const int32_t *list = reset_list(scratch);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         reset_wide(st, pool, ra, list[i], sh);
         __syncthreads();
@@ -868,6 +868,12 @@ extern "C" int sl_level_pool_prepare(sl_level_pool *pool, void *stream) {
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
+int sl::stream_offsets(const sl_env_state &st, const FastExtra &fx, hipStream_t s) {
+    const Scratch sc = scratch_of(fx.scratch, st.B);
+    return sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * st.B, fx.stream_pos, fx.stream_pos,
+                                 (void *)s);
+}
+
 extern "C" int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const uint8_t *mask,
                             const sl_env_cfg *cfg, void *stream) {
     if (!state_ok(st) || !pool || !cfg || pool->K <= 0 || pool->H != st->H || pool->W != st->W)
@@ -907,10 +913,13 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     a.draws = cfg->draws;
     a.n_draws = cfg->n_draws;
 
-    const bool philox_fast = cfg->rng_mode == SL_RNG_PHILOX && cfg->kernel != SL_KERNEL_GENERIC;
-    const bool fast = philox_fast && st->H == 64 && st->W == 64;
-    const bool fast128 = philox_fast && bits128_shape(*st);
-    const bool small = philox_fast && !fast && small_shape(*st);
+    if (cfg->rng_mode != SL_RNG_STREAM && cfg->rng_mode != SL_RNG_PHILOX) return SL_EINVAL;
+    const bool replay = cfg->rng_mode == SL_RNG_STREAM;
+    if (replay && (!cfg->stream_pos || (!cfg->draws && cfg->n_draws > 0))) return SL_EINVAL;
+    const bool bits_ok = cfg->kernel != SL_KERNEL_GENERIC;
+    const bool fast = bits_ok && st->H == 64 && st->W == 64;
+    const bool fast128 = bits_ok && bits128_shape(*st);
+    const bool small = bits_ok && !fast && small_shape(*st);
     if (cfg->kernel == SL_KERNEL_FAST && !fast && !fast128 && !small) return SL_ETOOBIG;
     bool reset_done = false;
     FastExtra fx;
@@ -926,6 +935,9 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
                 !info_flags || !cfg->auto_reset))
         return SL_EINVAL;
     fx.capture = cap;
+    fx.stream = replay ? 1 : 0;
+    fx.stream_pos = cfg->stream_pos;
+    fx.ev_begin = cfg->ev_begin;
     // the small-board kernel resets finished envs inside the step; with a capture the
     // resets run in the follow-up scan so the pre-reset frame can be copied first
     if (cap) fx.fuse_reset = 0;
@@ -943,21 +955,18 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     fx.obs_vw = cfg->obs_vw;
     fx.obs_rw = cfg->obs_remove_white;
     if (fast128) {
-        if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
         int rc = launch_step_bits128(*st, a, fx, actions, cfg->can_toggle_powers,
                                      cfg->can_toggle_colors, reward, done, info_flags, ep_len,
                                      ep_reward, s);
         if (rc) return rc;
         reset_done = fx.fuse_reset && fx.pool.K > 0;
     } else if (small) {
-        if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
         int rc = launch_step_small(*st, a, fx, actions, cfg->can_toggle_powers,
                                    cfg->can_toggle_colors, reward, done, info_flags, ep_len,
                                    ep_reward, s);
         if (rc) return rc;
         reset_done = fx.fuse_reset && fx.pool.K > 0 && fx.pool.H == st->H && fx.pool.W == st->W;
     } else if (fast) {
-        if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
         int rc = launch_step_bits(*st, a, fx, actions, cfg->can_toggle_powers,
                                   cfg->can_toggle_colors, reward, done, info_flags, ep_len,
                                   ep_reward, s);
@@ -967,8 +976,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         hipLaunchKernelGGL(k_env_action, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, *st,
                            actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act);
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
-        if (cfg->rng_mode == SL_RNG_STREAM) {
-            if (!cfg->stream_pos || (!cfg->draws && cfg->n_draws > 0)) return SL_EINVAL;
+        if (replay) {
             if (!set_lds((const void *)k_env_count, lds)) return SL_ETOOBIG;
             hipLaunchKernelGGL(k_env_count, dim3((unsigned)B), dim3(NT), lds, s, *st, sc.counts);
             if (hipGetLastError() != hipSuccess) return SL_EHIP;
@@ -979,14 +987,12 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
             hipLaunchKernelGGL(k_env_step_generic<SL_RNG_STREAM>, dim3((unsigned)B), dim3(NT), lds,
                                s, *st, a, sc.act, sc.offsets, sc.err, reward, done, info_flags,
                                ep_len, ep_reward);
-        } else if (cfg->rng_mode == SL_RNG_PHILOX) {
+        } else {
             if (!set_lds((const void *)k_env_step_generic<SL_RNG_PHILOX>, lds)) return SL_ETOOBIG;
             if (cfg->ev_begin) (void)hipEventRecord((hipEvent_t)cfg->ev_begin, s);
             hipLaunchKernelGGL(k_env_step_generic<SL_RNG_PHILOX>, dim3((unsigned)B), dim3(NT), lds,
                                s, *st, a, sc.act, sc.offsets, sc.err, reward, done, info_flags,
                                ep_len, ep_reward);
-        } else {
-            return SL_EINVAL;
         }
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;

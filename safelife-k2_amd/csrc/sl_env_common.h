@@ -6,12 +6,13 @@
 namespace sl {
 
 // scratch layout (int64 words), see sl_env_cfg.scratch (8*B + 16 words):
-//   [0, 2B)   per-(env, tensor) draw counts      (replay mode)
-//   [2B, 4B)  per-(env, tensor) stream offsets   (replay mode); in Philox mode the
-//             first B int32 slots hold the list of envs to reset after the step
-//             (64x64 and 128x128 kernels)
+//   [0, 2B)   per-(env, tensor) draw counts (replay mode; consumed by the scan before
+//             the step kernel runs); its first B int32 slots then hold the list of
+//             envs to reset after the step (64x64 and 128x128 kernels)
+//   [2B, 4B)  per-(env, tensor) stream offsets   (replay mode)
 //   [4B, 8B)  per env: action reward, d_points, d_score, d_side of the action's
-//             cell edits (the fast path keeps the scores incrementally)
+//             cell edits (the generic path; the bit-sliced replay prologues write
+//             the reward only)
 //   [8B]      error flags (bit0: draw stream exhausted)
 //   [8B+2], [8B+3]  reset-list lengths for even / odd steps (each step's reset
 //             kernel zeroes the other one)
@@ -21,6 +22,7 @@ struct Scratch {
 __host__ __device__ inline Scratch scratch_of(int64_t *s, int64_t B) {
     return Scratch{s, s + 2 * B, s + 4 * B, s + 8 * B};
 }
+__host__ __device__ inline int32_t *reset_list(int64_t *s) { return reinterpret_cast<int32_t *>(s); }
 
 struct StepArgs {
     int32_t time_limit, auto_reset, bonus_len, bonus_period;
@@ -247,7 +249,14 @@ struct FastExtra {
     int32_t obs_vh, obs_vw, obs_rw;   // board (NULL: none); view shape, remove_white
     const sl_capture *capture;        // trajectory capture (NULL: none): phase 0 is
                                       // launched between the step and reset kernels
+    int32_t stream;         // SL_RNG_STREAM: replay prologue (action + eligible counts),
+                            // offsets scan, then the step kernel's SPAWN_STREAM form
+    int64_t *stream_pos;    // replay mode: the stream position (in / out, device)
+    void *ev_begin;         // hipEvent_t recorded right before the step kernel, or NULL
 };
+// replay mode: exclusive scan of the prologue's per-(env, tensor) eligible counts into
+// each tensor's first uniform, advancing *fx.stream_pos (sl_env.hip)
+int stream_offsets(const sl_env_state &st, const FastExtra &fx, hipStream_t s);
 // copies of the captured envs' state (sl_capture): phase 0 after the advance (and
 // the step's flags), phase 1 after the resets
 int launch_capture(const sl_env_state &st, const sl_capture &c, const uint8_t *flags, int phase,

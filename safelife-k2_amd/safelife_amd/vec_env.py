@@ -190,9 +190,13 @@ class SafeLifeVecEnv:
         self.st_t["start_roll"].fill_(-1)
 
     def set_spawn_stream(self, stream, pos=0):
-        """Uniform doubles consumed in reference order (rng='stream')."""
+        """Uniform doubles consumed in reference order (rng='stream'): a numpy array,
+        or a float64 tensor (used in place when it is already on this device)."""
         torch = self.torch
-        s = torch.as_tensor(np.ascontiguousarray(stream, dtype=np.float64)).to(self.device)
+        if isinstance(stream, torch.Tensor):
+            s = stream.to(device=self.device, dtype=torch.float64).contiguous()
+        else:
+            s = torch.as_tensor(np.ascontiguousarray(stream, dtype=np.float64)).to(self.device)
         self.spawn_stream = s
         self.stream_pos.fill_(int(pos))
 

@@ -39,24 +39,26 @@ def test_labels():
     assert bench.metric_name(64, 64, 65536) == json.load(
         open(os.path.join(REPO, "BASELINE.json")))["metric"]
     assert "25×25" in bench.metric_name(25, 25, 4096)
-    assert bench.step_kernel_name(64, 64, "none", "auto") == "k_env_step_bits64<false>"
-    assert bench.step_kernel_name(64, 64, "packed", "auto") == "k_env_step_bits64<true>"
-    assert bench.step_kernel_name(25, 25, "none", "auto") == "k_env_step_small"
-    assert bench.step_kernel_name(128, 128, "none", "auto") == "k_env_step_bits128"
+    assert bench.step_kernel_name(64, 64, "none", "auto") == "k_env_step_bits64<false, 0>"
+    assert bench.step_kernel_name(64, 64, "packed", "auto") == "k_env_step_bits64<true, 0>"
+    assert bench.step_kernel_name(25, 25, "none", "auto") == "k_env_step_small<0>"
+    assert bench.step_kernel_name(128, 128, "none", "auto") == "k_env_step_bits128<0>"
+    assert (bench.step_kernel_name(128, 128, "none", "auto", "stream")
+            == "k_env_step_bits128<1>")
     assert bench.step_kernel_name(64, 64, "none", "generic") == "k_env_step_generic"
 
 
 def test_pmc_record_keyed_on_build(tmp_path, monkeypatch):
     prof = tmp_path / "profiles"
     prof.mkdir()
-    rec = {"kernel": "void k_env_step_bits64<false>(StepKArgs)", "build_id": "abc",
+    rec = {"kernel": "void k_env_step_bits64<false, 0>(StepKArgs)", "build_id": "abc",
            "hbm_bytes_per_launch": 123.0, "profile": "rX"}
     (prof / "pmc_c3.json").write_text(json.dumps(rec))
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
-    assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits64<false>")[0] == 123.0
-    assert bench.traffic_from_record("c3", "none", "other", "k_env_step_bits64<false>")[0] is None
-    assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits128")[0] is None
-    assert bench.traffic_from_record("c5", "none", "abc", "k_env_step_bits128")[0] is None
+    assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits64<false, 0>")[0] == 123.0
+    assert bench.traffic_from_record("c3", "none", "other", "k_env_step_bits64<false, 0>")[0] is None
+    assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits128<0>")[0] is None
+    assert bench.traffic_from_record("c5", "none", "abc", "k_env_step_bits128<0>")[0] is None
 
 
 def test_build_id_file_matches_library():

@@ -127,11 +127,14 @@ def _vec_env_from_traj(d, B=1, **kw):
     return SafeLifeVecEnv(pool, B, "cuda:0", **args)
 
 
+@pytest.mark.parametrize("kernel", ["fast", "generic"])
 @pytest.mark.parametrize("path", _traj_files(), ids=lambda p: os.path.basename(p)[5:-4])
-def test_env_golden_trajectory(torch_dev, path):
+def test_env_golden_trajectory(torch_dev, path, kernel):
+    """The reference-captured trajectories (reference-order spawn stream) through the
+    bit-sliced kernels (replay prologue + SPAWN_STREAM step) and the per-cell kernel."""
     torch, dev = torch_dev
     d = np.load(path)
-    env = _vec_env_from_traj(d)
+    env = _vec_env_from_traj(d, kernel=kernel)
     obs = env.reset().cpu().numpy()
     assert np.array_equal(obs[0], d["obs0"])
     T = len(d["action"])
