@@ -241,8 +241,8 @@ def side_effect_densities(init_board, final_board, num_steps, spawn_prob, num_sa
     """The rollout of side_effect_score (side_effects.py:131-139): b0 from the initial
     board advanced num_steps times, then num_samples x (b0, b1) advances, each pair
     added to its density map.  rng 'stream' draws from stream.take() in the
-    reference's order; 'philox' keys a draw on (cell, env_id, advance index of that
-    board, 4 + board)."""
+    reference's order; 'philox' keys a draw on (2x2 block of the cell, env_id, advance
+    index of that board, 4 + board) -- orc_spawn_uniform."""
     b0 = np.array(init_board, dtype=np.uint16)
     b1 = np.array(final_board, dtype=np.uint16)
     inaction, action = {"n": 0}, {"n": 0}

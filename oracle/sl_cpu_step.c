@@ -37,6 +37,8 @@ int orc_advance(const uint16_t *in, uint16_t *out, int H, int W, float p, int rn
                 uint32_t env_id, uint32_t step, uint32_t tensor);
 double orc_philox_uniform(uint32_t cell, uint32_t env, uint32_t step, uint32_t tensor,
                           uint64_t seed);
+double orc_spawn_uniform(int y, int x, int W, uint32_t env, uint32_t step, uint32_t tensor,
+                         uint64_t seed);
 
 #define C_ALIVE 0x0001u
 #define C_AGENT 0x0002u
@@ -211,7 +213,7 @@ static void fast_advance(const uint16_t *in, uint16_t *out, int H, int W, float 
                             col |= 0x200u << k;
                     if (cnt == 3)
                         r = (uint16_t)(C_ALIVE | col | (((n >> 4) & 15u) >= 2 ? C_DESTR : 0u));
-                    else if (orc_philox_uniform((uint32_t)(y * W + x), env, step, tensor, seed) < thr)
+                    else if (orc_spawn_uniform(y, x, W, env, step, tensor, seed) < thr)
                         r = (uint16_t)(C_ALIVE | C_DESTR | col);
                 }
             }

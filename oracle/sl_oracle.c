@@ -74,6 +74,18 @@ double orc_philox_uniform(uint32_t cell, uint32_t env, uint32_t step,
     return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
 }
 
+/* Philox-mode spawn draw of cell (y, x) of a W-column tensor (the build's own RNG; the
+   reference has only its global stream): the four cells of the 2x2 block
+   (y >> 1, x >> 1) share one Philox4x32-10 evaluation, counter (block, env, step,
+   tensor) with block = (y >> 1) * ceil(W / 2) + (x >> 1); cell (y, x) takes output
+   word (y & 1) * 2 + (x & 1), as word * 2^-32.  Same as spawn_uniform (sl_device.h). */
+double orc_spawn_uniform(int y, int x, int W, uint32_t env, uint32_t step, uint32_t tensor,
+                         uint64_t seed) {
+    uint32_t r[4];
+    orc_philox4x32(r, (uint32_t)((y >> 1) * ((W + 1) >> 1) + (x >> 1)), env, step, tensor, seed);
+    return (double)r[(y & 1) * 2 + (x & 1)] * (1.0 / 4294967296.0);
+}
+
 /* ---------------- per-cell rule (Appendix A) ---------------- */
 typedef struct {
     int cnt;          /* alive cells in 3x3 incl. self, with multiplicity */
@@ -153,8 +165,7 @@ int orc_advance(const uint16_t *in, uint16_t *out, int H, int W, float p,
             } else if (n.any_s) {
                 double u;
                 if (rng_mode == ORC_RNG_PHILOX) {
-                    u = orc_philox_uniform((uint32_t)(y * W + x), env_id, step,
-                                           tensor, seed);
+                    u = orc_spawn_uniform(y, x, W, env_id, step, tensor, seed);
                 } else if (draws == NULL) {
                     if (!(thr <= 0.0 || thr >= 1.0)) return -1;
                     u = thr <= 0.0 ? 1.0 : 0.0;

@@ -11,7 +11,8 @@
 //                    the planes), including the rows just outside the word;
 //   g.horiz(w0, w1)  columns col0-1 / col0+2 of a per-word quantity;
 //   g.halo_spawn()   a spawner sits in a row just outside the wave's words;
-//   g.cell(y, w)     the cell's flat index (the Philox counter of its draw);
+//   g.block(y)       the 2x2 spawn block holding rows y, y + 1 of the lane's two
+//                    columns (the Philox counter of their draws, spawn_uniform);
 //   g.spawn(...)     the spawns among the eligible cells (SPAWN_PHILOX / _STREAM /
 //                    _COUNT below).
 #pragma once
@@ -156,23 +157,28 @@ struct StreamSrc {
     int64_t *err;
 };
 
-// Spawn draws of the eligible cells elig[w] (bit y of word w), one lane at a time:
-// sp[w] gets the cells whose uniform is below the threshold.  A wave takes as many
-// Philox evaluations as its busiest lane has eligible cells.
+// Philox spawn draws of the eligible cells elig[w] (bit y of word w), per lane: the
+// lane's two columns over rows y, y + 1 (y even) are one 2x2 block, one Philox
+// evaluation (spawn_uniform, sl_device.h).  sp[w] gets the eligible cells whose
+// uniform is below the threshold.  A wave takes as many evaluations as its busiest
+// lane has blocks holding an eligible cell (the words' rows start at an even row).
 template <class Geo>
 __device__ __forceinline__ void lane_draws(const Geo &g, const u32 elig[2], u32 sp[2],
                                            const SpawnCtx &sc, u32 tensor) {
-#pragma unroll
-    for (int w = 0; w < 2; w++) {
-        u32 e = elig[w], s = 0;
-        while (e) {
-            const int y = __builtin_ctz(e);
-            e &= e - 1;
-            if (philox_uniform(g.cell(y, w), sc.gid, sc.step, tensor, sc.seed) < sc.thr)
-                s |= 1u << y;
-        }
-        sp[w] = s;
+    // word * 2^-32 < thr  <=>  word <= ceil(thr * 2^32) - 1 (0 < thr < 1; both exact)
+    const u32 lim = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(ceil(sc.thr * 4294967296.0) - 1.0));
+    const u32 any = elig[0] | elig[1];
+    u32 blocks = (any | (any >> 1)) & 0x55555555u, s0 = 0u, s1 = 0u;
+    while (blocks) {
+        const int y = __builtin_ctz(blocks);
+        blocks &= blocks - 1;
+        uint32_t r[4];
+        philox4x32(g.block(y), sc.gid, sc.step, tensor, sc.seed, r);
+        s0 |= ((r[0] <= lim ? 1u : 0u) | (r[2] <= lim ? 2u : 0u)) << y;
+        s1 |= ((r[1] <= lim ? 1u : 0u) | (r[3] <= lim ? 2u : 0u)) << y;
     }
+    sp[0] = s0 & elig[0];
+    sp[1] = s1 & elig[1];
 }
 template <class Geo>
 __device__ __forceinline__ void philox_spawn(const Geo &g, const u32 elig[2], u32 sp[2],

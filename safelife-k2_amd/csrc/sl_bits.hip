@@ -64,8 +64,9 @@ struct Geo64 {
         return H3{lane_m1(lane_m1(w1)), lane_p1(lane_p1(w0))};
     }
     __device__ __forceinline__ bool halo_spawn() const { return false; }
-    __device__ __forceinline__ u32 cell(int y, int w) const {
-        return (u32)((32 * (lane & 1) + y) * N + 2 * (lane >> 1) + w);
+    // the 2x2 spawn block of rows 32h + y, y + 1 (y even) of the lane's column pair
+    __device__ __forceinline__ u32 block(int y) const {
+        return (u32)(((32 * (lane & 1) + y) >> 1) * (N / 2) + (lane >> 1));
     }
     // spawners are rare on these boards: per-lane Philox draws, no LDS list
     __device__ __forceinline__ void spawn(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,

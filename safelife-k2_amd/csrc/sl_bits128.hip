@@ -79,9 +79,9 @@ struct GeoBand {
     __device__ __forceinline__ bool halo_spawn() const {
         return (PL(hv, 7, 0) | PL(hv, 7, 1)) != 0u;
     }
-    __device__ __forceinline__ u32 cell(int y, int w) const { return cell_at(lane, y, w); }
-    __device__ __forceinline__ u32 cell_at(int l, int y, int w) const {
-        return (u32)((row0 + y) * N + 2 * l + w);
+    // the 2x2 spawn block of band rows y, y + 1 (y even) of the lane's column pair
+    __device__ __forceinline__ u32 block(int y) const {
+        return (u32)(((row0 + y) >> 1) * (N / 2) + lane);
     }
     __device__ __forceinline__ void spawn(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
                                           u32 tensor) {
@@ -94,11 +94,6 @@ struct GeoBand {
         }
     }
 };
-
-// the halo rows of band t from the eight preloaded ones (t is wave-uniform)
-__device__ __forceinline__ u32 pick4(const u32 h[4], int t) {
-    return t == 0 ? h[0] : t == 1 ? h[1] : t == 2 ? h[2] : h[3];
-}
 
 // Applies the action's cell edits (wave-uniform (flat index, value) pairs) to band
 // t's planes on the lane owning the cell; returns the band rows (bit y) edited.
@@ -201,17 +196,17 @@ __device__ __forceinline__ const Step128KArgs &kargs128() {
     return *(const Step128KArgs *)kp;
 }
 
-// MODE: SPAWN_PHILOX, or SPAWN_STREAM (replay: k_stream_prologue128 has run the action
-// and sized the draws; the step reads act[b] and each tensor's first uniform from the
-// scratch words)
+// One env-step of env b, after the action: k_env_action (Philox mode) or
+// k_stream_prologue128 (replay) has applied it -- state and cell edits in HBM, reward
+// in scratch act[b] -- so this kernel holds no action code, no edit lists and no
+// overlay.  MODE: SPAWN_PHILOX, or SPAWN_STREAM (each tensor's first uniform from the
+// scratch offsets).
 template <int MODE>
 __global__ void __launch_bounds__(64, kMinWaves)
 k_env_step_bits128(Step128KArgs ka) {
     const sl_env_state &st = ka.st;
     const StepArgs &a = ka.a;
     const FastExtra &fx = ka.fx;
-    const int32_t *__restrict__ actions = ka.actions;
-    const int ctp = ka.ctp, ctc = ka.ctc;
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x;
     const int64_t off = b * (int64_t)(N * N);
@@ -220,17 +215,11 @@ k_env_step_bits128(Step128KArgs ka) {
     const u32 *gs = reinterpret_cast<const u32 *>(st.start_board + off) + lane;
     u32 *mg = st.planes + b * (int64_t)(NB * MW) + lane;            // mirror [t][q][lane]
 
-    const u32 V = load_record(st, actions, b, lane);
+    const u32 V = load_record(st, ka.actions, b, lane);
     __shared__ __attribute__((aligned(16))) u32 spool_[kPoolPlanes * 256];
     __attribute__((address_space(3))) u32 *spool = (__attribute__((address_space(3))) u32 *)spool_;
-    // pre-step halo rows of every band: above (32t - 1) and below (32t + 32)
-    u32 bu[NB], bd[NB];
-#pragma unroll
-    for (int t = 0; t < NB; t++) {
-        bu[t] = gb[((32 * t - 1) & (N - 1)) * RS];
-        bd[t] = gb[((32 * t + 32) & (N - 1)) * RS];
-    }
     const int pok = rec(V, R_POK) & 6;
+    const Scratch w = scratch_of(fx.scratch, st.B);
 
     SpawnCtx sc;
     sc.gid = a.env0 + (uint32_t)b;
@@ -240,44 +229,46 @@ k_env_step_bits128(Step128KArgs ka) {
     StreamSrc ssrc{a.draws, a.n_draws, nullptr};
     int64_t pos_b = 0, pos_g = 0;
     if (MODE == SPAWN_STREAM) {
-        const Scratch w = scratch_of(fx.scratch, st.B);
         ssrc.err = w.err;
         pos_b = w.offsets[2 * b];
         pos_g = w.offsets[2 * b + 1];
     }
+    // Bands are processed in order 0..3, so the pre-step halo rows of band t are band
+    // t - 1's last row (kept from its load: it is written back before band t runs),
+    // and band t + 1's first row (not yet written); band 3's lower halo is row 0,
+    // kept from band 0's load, and band 0's upper halo is row 127, read up front.
 
     // ---- goals: advanced band by band unless at a fixed point; the mirror keeps
     // their planes (all words rewritten when it was stale, else the changed ones)
     if ((pok & 6) != 6) {
-        u32 gu[NB], gd[NB];
-#pragma unroll
-        for (int t = 0; t < NB; t++) {
-            gu[t] = gg[((32 * t - 1) & (N - 1)) * RS];
-            gd[t] = gg[((32 * t + 32) & (N - 1)) * RS];
-        }
         const bool all = !(pok & 2);
         u32 changed = 0, spawners = 0;
+        u32 up = gg[(N - 1) * RS], row0 = 0;
 #pragma unroll 1
         for (int t = 0; t < NB; t++) {
             u32 G[32];
             load_pairs<RS>(gg + 32 * t * RS, G);
+            const u32 dn = t < NB - 1 ? gg[(32 * t + 32) * RS] : row0;
+            if (t == 0) row0 = G[0];
+            const u32 last = G[31];
             transpose32(G);
             u32 cg[2];
-            GeoBand<MODE> geo{lane, 32 * t, HaloView{pick4(gu, t), pick4(gd, t)}, ssrc, pos_g, 0, 0};
+            GeoBand<MODE> geo{lane, 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_g, 0, 0};
             rule_planes(G, cg, geo, sc, 1u);
             pos_g += geo.used;
+            up = last;
             const u32 rg = wave_or(cg[0] | cg[1]);
             u32 *m = mg + t * MW;       // only the colour planes are ever read back
 #pragma unroll
-            for (int w = 0; w < 2; w++)
-                if (all || cg[w])
+            for (int q = 0; q < 2; q++)
+                if (all || cg[q])
 #pragma unroll
-                    for (int k = 9; k < 12; k++) m[(k + 16 * w) * 64] = PL(G, k, w);
+                    for (int k = 9; k < 12; k++) m[(k + 16 * q) * 64] = PL(G, k, q);
             changed |= rg;
             spawners |= PL(G, 7, 0) | PL(G, 7, 1);
             if (rg) {
-                transpose32(G);
                 const u32 lm = sector_rows(cg[0] | cg[1]);
+                transpose32(G);
 #pragma unroll
                 for (int y = 0; y < 32; y++)
                     if ((rg >> y) & 1u)
@@ -291,48 +282,15 @@ k_env_step_bits128(Step128KArgs ka) {
     }
     __builtin_amdgcn_sched_barrier(0);
 
-    // ---- the action (lane 0) on the pre-step board
-    OverlayT<GlobalCells> ov;
-    ov.src.bd = st.board + off;
-    ov.n = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        ov.idx[k] = 0;
-        ov.val[k] = 0;
-    }
-    RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
-               rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
-    int act_reward = 0;
-    if (MODE == SPAWN_STREAM) {        // the prologue ran the action (no edits left)
-        act_reward = (int)scratch_of(fx.scratch, st.B).act[b];
-    } else {
-        if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ctp, ctc, ov);
-        act_reward = __builtin_amdgcn_readfirstlane(act_reward);
-    }
-    const int ne = __builtin_amdgcn_readfirstlane(ov.n);
-    int eidx[4];
-    u32 eval[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        eidx[k] = __builtin_amdgcn_readfirstlane(ov.idx[k]);
-        eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
-    }
-    RecFields fl{V, __builtin_amdgcn_readfirstlane(env.go), __builtin_amdgcn_readfirstlane(env.ax),
-                 __builtin_amdgcn_readfirstlane(env.ay), 0.0};
+    const int act_reward = (int)w.act[b];
+    RecFields fl{V, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), 0.0};
     if (a.bonus_period > 0)        // issued now, consumed by the epilogue
         fl.bval = a.bonus_table[bonus_dist(fl.ax, fl.ay, fl.prior_x(fl.prior_head()),
                                            fl.prior_y(fl.prior_head()), fl.prior_len(),
                                            a.bonus_period, a.bonus_len)];
-    if (ne > 0) {
-#pragma unroll
-        for (int t = 0; t < NB; t++) {
-            bu[t] = edit_row(bu[t], (32 * t - 1) & (N - 1), ne, eidx, eval, lane);
-            bd[t] = edit_row(bd[t], (32 * t + 32) & (N - 1), ne, eidx, eval, lane);
-        }
-    }
 
-    // ---- board, band by band: rule, scores, changed rows back.  The start board
-    // comes from the level pool's planes when the env was reset from the pool
+    // ---- board, band by band: rule, scores, changed sectors back.  The start board
+    // comes from the level pool's planes when the env was reset from it
     // (start_roll = (dy << 16) | dx), else from HBM (written by the caller).
     const sl_level_pool &pool = fx.pool;
     const int roll = (pool.board_planes && pool.K > 0 && pool.H == N &&
@@ -343,28 +301,25 @@ k_env_step_bits128(Step128KArgs ka) {
     const int sdy = roll >> 16, sdx = roll & 0xFFFF;
     const int sc0 = (2 * lane - sdx) & (N - 1), sc1 = (sc0 + 1) & (N - 1);
     int pts = 0, scr = 0, pos = 0, side = 0;
+    u32 up = gb[(N - 1) * RS], row0 = 0;
 #pragma unroll 1
     for (int t = 0; t < NB; t++) {
-        u32 P[32], S[32];
+        u32 P[32];
         load_pairs<RS>(gb + 32 * t * RS, P);
+        const u32 dn = t < NB - 1 ? gb[(32 * t + 32) * RS] : row0;
         if (roll >= 0) {
             wait_lgkm();        // the previous band's reads of the buffer are done
             pool_dma128(pp, t, sdy, lane, spool);
         }
+        if (t == 0) row0 = P[0];
+        const u32 last = P[31];
         transpose32(P);
-        const u32 erow = apply_edits(P, ne, eidx, eval, 32 * t, lane);
         u32 cb[2];
-        GeoBand<MODE> geo{lane, 32 * t, HaloView{pick4(bu, t), pick4(bd, t)}, ssrc, pos_b, 0, 0};
+        GeoBand<MODE> geo{lane, 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_b, 0, 0};
         rule_planes(P, cb, geo, sc, 0u);
         pos_b += geo.used;
+        up = last;
         __builtin_amdgcn_sched_barrier(0);
-        if (roll < 0) {
-            load_pairs<RS>(gs + 32 * t * RS, S);
-            transpose32(S);
-        } else {
-            wait_vm();          // the band's pool planes have landed in LDS
-            pool_start_lds(spool, t, sdy, sc0, sc1, S);
-        }
         u32 gcol[3][2];
         const u32 *m = mg + t * MW;
 #pragma unroll
@@ -373,17 +328,25 @@ k_env_step_bits128(Step128KArgs ka) {
             gcol[k][1] = m[(25 + k) * 64];
         }
         int p, q, r, e;
+        u32 S[32];
+        if (roll < 0) {
+            load_pairs<RS>(gs + 32 * t * RS, S);
+            transpose32(S);
+        } else {
+            wait_vm();          // the band's pool planes have landed in LDS
+            pool_start_lds(spool, t, sdy, sc0, sc1, S);
+        }
         score_planes(P, gcol, S, &p, &q, &r, &e);
         pts += p;
         scr += q;
         pos += r;
         side += e;
-        const u32 rb = wave_or(cb[0] | cb[1]) | erow;
+        const u32 rb = wave_or(cb[0] | cb[1]);
         if (rb) {
-            transpose32(P);
             // only the changed 64-byte row sectors (inline: as a helper call the
             // compiler gives this kernel 30 more VGPRs and drops it to 2 waves/SIMD)
-            const u32 lm = sector_rows(cb[0] | cb[1]) | erow;
+            const u32 lm = sector_rows(cb[0] | cb[1]);
+            transpose32(P);
 #pragma unroll
             for (int y = 0; y < 32; y++)
                 if ((rb >> y) & 1u)
@@ -500,6 +463,8 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
         hipLaunchKernelGGL(k_env_step_bits128<SPAWN_STREAM>, grid, dim3(64), 0, s, ka);
     } else {
+        const int rc = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
+        if (rc) return rc;
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
         hipLaunchKernelGGL(k_env_step_bits128<SPAWN_PHILOX>, grid, dim3(64), 0, s, ka);
     }

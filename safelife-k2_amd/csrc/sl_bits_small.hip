@@ -53,7 +53,8 @@ struct GeoSmall {
                   (u32)__builtin_amdgcn_ds_bpermute(4 * src_r, (int)w0)};
     }
     __device__ __forceinline__ bool halo_spawn() const { return false; }
-    __device__ __forceinline__ u32 cell(int y, int w) const { return (u32)(y * W + 2 * lane + w); }
+    // the 2x2 spawn block of rows y, y + 1 (y even) of the lane's column pair
+    __device__ __forceinline__ u32 block(int y) const { return (u32)((y >> 1) * nl + lane); }
     // (the column-0 copy's draws are discarded with the rest of that word; in replay
     // mode it draws nothing, so it cannot shift the real cells' ranks)
     __device__ __forceinline__ void spawn(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,

@@ -88,7 +88,8 @@ k_advance(const uint16_t *__restrict__ in, uint16_t *__restrict__ out, int H, in
             }
             pos += tot;
         } else if (elig) {
-            u = philox_uniform((uint32_t)i, env0 + (uint32_t)b, step, tensor, seed);
+            const int y = i / W;
+            u = spawn_uniform(y, i - y * W, W, env0 + (uint32_t)b, step, tensor, seed);
         }
         if (elig && u < thr) r = sv;
         if (i < hw) dst[i] = (uint16_t)r;
@@ -202,7 +203,8 @@ k_rollout_advance(const uint16_t *__restrict__ in, uint16_t *__restrict__ out, i
             if (elig) u = draws[pos + rank];
             pos += tot;
         } else if (elig) {
-            u = philox_uniform((uint32_t)i, env0 + (uint32_t)e, t, 4u + (uint32_t)which, seed);
+            const int y = i / W;
+            u = spawn_uniform(y, i - y * W, W, env0 + (uint32_t)e, t, 4u + (uint32_t)which, seed);
         }
         if (elig && u < thr) r = sv;
         if (i < hw) dst[i] = (uint16_t)r;

@@ -24,10 +24,12 @@ constexpr uint32_t POWERS = ALIVE | INHIBIT | PRESERVE | SPAWN;
 // ----------------------------------------------------------------------------
 // Philox4x32-10, counter (c0..c3), key = seed.  Identical to oracle/sl_oracle.c.
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ double philox_uniform(uint32_t c0, uint32_t c1, uint32_t c2,
-                                                 uint32_t c3, uint64_t seed) {
+__device__ __forceinline__ void philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                           uint64_t seed, uint32_t out[4]) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#pragma unroll
+    // rolled: unrolled inside the bit-sliced kernels' draw loops it costs the 64x64
+    // kernel 64 spilled VGPRs
+#pragma unroll 1
     for (int r = 0; r < 10; r++) {
         uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
         uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
@@ -37,8 +39,39 @@ __device__ __forceinline__ double philox_uniform(uint32_t c0, uint32_t c1, uint3
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
-    uint32_t a = c0 >> 5, b = c1 >> 6;
+    out[0] = c0;
+    out[1] = c1;
+    out[2] = c2;
+    out[3] = c3;
+}
+
+// a uniform double in [0,1) with 53 random bits (numpy's construction) from one
+// evaluation: level choices, rolls and action samples
+__device__ __forceinline__ double philox_uniform(uint32_t c0, uint32_t c1, uint32_t c2,
+                                                 uint32_t c3, uint64_t seed) {
+    uint32_t x[4];
+    philox4x32(c0, c1, c2, c3, seed, x);
+    uint32_t a = x[0] >> 5, b = x[1] >> 6;
     return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+}
+
+// Philox-mode spawn draws (the build's own throughput RNG; the reference has only its
+// global stream, replayed by SL_RNG_STREAM).  The four cells of the 2x2 block
+// (y >> 1, x >> 1) share one evaluation, counter (block, env, step, tensor) with
+// block = (y >> 1) * ceil(W / 2) + (x >> 1); cell (y, x) takes output word
+// (y & 1) * 2 + (x & 1) as the uniform word * 2^-32 (exact in a double), so a
+// clustered group of eligible cells costs a quarter of the Philox work.
+__device__ __forceinline__ uint32_t spawn_block(int y, int x, int W) {
+    return (uint32_t)((y >> 1) * ((W + 1) >> 1) + (x >> 1));
+}
+__device__ __forceinline__ double spawn_word_uniform(uint32_t w) {
+    return (double)w * (1.0 / 4294967296.0);
+}
+__device__ __forceinline__ double spawn_uniform(int y, int x, int W, uint32_t env, uint32_t step,
+                                                uint32_t tensor, uint64_t seed) {
+    uint32_t r[4];
+    philox4x32(spawn_block(y, x, W), env, step, tensor, seed, r);
+    return spawn_word_uniform(r[(y & 1) * 2 + (x & 1)]);
 }
 
 // ----------------------------------------------------------------------------

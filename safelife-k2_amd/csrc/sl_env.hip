@@ -49,15 +49,17 @@ __device__ __forceinline__ void cell_terms(uint32_t bv, uint32_t gv, uint32_t sv
     *se = side_term(bv, sv, gv);
 }
 
-// The action edits at most the 4 cells agent / front / behind / two ahead; their
-// contribution to the running scores is re-evaluated here (pre vs post edit) so the
-// fast step kernel can keep points / score / side effects incrementally.
+// The action edits at most the 4 cells agent / front / behind / two ahead.  DELTAS:
+// their contribution to the running scores is re-evaluated too (pre vs post edit, act
+// words 1-3), and the goals mirror is marked stale (the per-cell path does not keep
+// it); without DELTAS only the reward is written (the 128x128 kernel's pre-pass).
+template <bool DELTAS>
 __global__ void __launch_bounds__(256)
 k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int ctc,
              int64_t *__restrict__ act) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= st.B) return;
-    if (st.planes_ok) st.planes_ok[b] = 0;    // this path does not keep the 64x64 mirror
+    if (DELTAS && st.planes_ok) st.planes_ok[b] = 0;
     const int H = st.H, W = st.W;
     const int64_t hw = (int64_t)H * W;
     uint16_t *bd = st.board + b * hw;
@@ -79,12 +81,13 @@ k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int 
             uniq[k] = true;
             for (int j = 0; j < k; j++) uniq[k] = uniq[k] && cells[j] != cells[k];
         }
-        for (int k = 0; k < 4; k++)
-            if (uniq[k]) {
-                int p, q, se;
-                cell_terms(bd[cells[k]], gd[cells[k]], sd[cells[k]], &p, &q, &se);
-                d_pts -= p; d_scr -= q; d_side -= se;
-            }
+        if (DELTAS)
+            for (int k = 0; k < 4; k++)
+                if (uniq[k]) {
+                    int p, q, se;
+                    cell_terms(bd[cells[k]], gd[cells[k]], sd[cells[k]], &p, &q, &se);
+                    d_pts -= p; d_scr -= q; d_side -= se;
+                }
         if (a <= 4) {
             // move_agent(1)
             const int x2 = pymod(x0 - fx, W), y2 = pymod(y0 - fy, H);
@@ -133,17 +136,20 @@ k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int 
                 bd[y0 * W + x0] = (uint16_t)(bd[y0 * W + x0] ^ (t & tb));
             }
         }
-        for (int k = 0; k < 4; k++)
-            if (uniq[k]) {
-                int p, q, se;
-                cell_terms(bd[cells[k]], gd[cells[k]], sd[cells[k]], &p, &q, &se);
-                d_pts += p; d_scr += q; d_side += se;
-            }
+        if (DELTAS)
+            for (int k = 0; k < 4; k++)
+                if (uniq[k]) {
+                    int p, q, se;
+                    cell_terms(bd[cells[k]], gd[cells[k]], sd[cells[k]], &p, &q, &se);
+                    d_pts += p; d_scr += q; d_side += se;
+                }
     }
     act[b] = reward;
-    act[st.B + b] = d_pts;
-    act[2 * st.B + b] = d_scr;
-    act[3 * st.B + b] = d_side;
+    if (DELTAS) {
+        act[st.B + b] = d_pts;
+        act[2 * st.B + b] = d_scr;
+        act[3 * st.B + b] = d_side;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -279,8 +285,9 @@ k_env_step_generic(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
             pos_b += tb;
             pos_g += tg;
         } else {
-            if (eb) ub = philox_uniform((uint32_t)i, a.env0 + (uint32_t)b, a.step, 0u, a.seed);
-            if (eg) ug = philox_uniform((uint32_t)i, a.env0 + (uint32_t)b, a.step, 1u, a.seed);
+            const int y = i / W, x = i - y * W;
+            if (eb) ub = spawn_uniform(y, x, W, a.env0 + (uint32_t)b, a.step, 0u, a.seed);
+            if (eg) ug = spawn_uniform(y, x, W, a.env0 + (uint32_t)b, a.step, 1u, a.seed);
         }
         if (eb && ub < thr) nb = sb;
         if (eg && ug < thr) ng = sg;
@@ -810,6 +817,13 @@ int launch_obs(const sl_env_state &st, const ObsArgs &a, void *out, hipStream_t 
 }  // namespace
 
 namespace sl {
+int launch_env_action(const sl_env_state &st, const int32_t *actions, int ctp, int ctc,
+                      int64_t *act, hipStream_t s) {
+    hipLaunchKernelGGL(k_env_action<false>, dim3((unsigned)((st.B + 255) / 256)), dim3(256), 0,
+                       s, st, actions, ctp, ctc, act);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
 int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
                            int64_t *scratch, uint32_t step, hipStream_t s) {
     const unsigned grid = (unsigned)(st.B < 256 ? st.B : 256);
@@ -973,8 +987,8 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         if (rc) return rc;
         reset_done = fx.fuse_reset && fx.pool.K > 0;
     } else {
-        hipLaunchKernelGGL(k_env_action, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, *st,
-                           actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act);
+        hipLaunchKernelGGL(k_env_action<true>, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s,
+                           *st, actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act);
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
         if (replay) {
             if (!set_lds((const void *)k_env_count, lds)) return SL_ETOOBIG;

@@ -274,6 +274,10 @@ int launch_step_small(const sl_env_state &st, const StepArgs &a, const FastExtra
 int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                         const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                         uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
+// the action of every env (k_env_action, one lane per env): state and cell edits in
+// HBM, reward into act[b]; the 128x128 kernel's pre-pass (sl_env.hip)
+int launch_env_action(const sl_env_state &st, const int32_t *actions, int ctp, int ctc,
+                      int64_t *act, hipStream_t s);
 // resets of the envs queued in the scratch list for step `step`, one 1024-thread
 // block each (sl_env.hip)
 int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
