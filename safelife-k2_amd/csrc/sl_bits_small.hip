@@ -442,6 +442,445 @@ k_env_step_small(SmallKArgs ka) {
     }
 }
 
+// ============================================================================
+// Four envs per wave (boards up to 32 x 32: C2's 25x25 proc-gen levels, the 26x26
+// v1.0 benchmark levels).  The layout above uses nl = ceil(W/2) <= 16 lanes of 64 on
+// such boards; here env e of the wave (global env 4 * blockIdx + e) owns lanes
+// 16e .. 16e+15 -- one DPP row -- so each wave64 instruction advances four boards.
+// Per-env sums and masks are DPP row reductions (seg_total / seg_or), horizontal
+// neighbours stay ds_bpermute within the segment, the per-env record is four
+// registers (lane 16e + k of register q = field 16q + k of env e, fetched with
+// ds_bpermute), and the action and epilogue run on each segment's first lane.  Exits
+// are coloured in the planes (their rows stored when the colour changes), so the
+// epilogue writes no cells.  Envs whose episode ended are reset one at a time by the
+// whole wave (small_reset).
+// ============================================================================
+constexpr int kSegW = 32;            // widest board
+
+__device__ __forceinline__ u32 seg_or(u32 v) {          // OR over the lane's DPP row
+    v |= dpp<0x121>(v);    // row_ror:1
+    v |= dpp<0x122>(v);    // row_ror:2
+    v |= dpp<0x124>(v);    // row_ror:4
+    v |= dpp<0x128>(v);    // row_ror:8
+    return v;
+}
+__device__ __forceinline__ int seg_total(int x) {        // sum over the lane's DPP row
+    u32 v = (u32)x;
+    v += dpp<0x121>(v);
+    v += dpp<0x122>(v);
+    v += dpp<0x124>(v);
+    v += dpp<0x128>(v);
+    return (int)v;
+}
+
+// Spawn draws with per-lane env parameters (each segment is another env): Philox
+// blocks as lane_draws, with the lane's own threshold.
+template <class Geo>
+__device__ __forceinline__ void seg_philox(const Geo &g, const u32 elig[2], u32 sp[2],
+                                           const SpawnCtx &sc, u32 tensor) {
+    sp[0] = 0u;
+    sp[1] = 0u;
+    if (sc.thr >= 1.0) {
+        sp[0] = elig[0];
+        sp[1] = elig[1];
+    } else if (sc.thr > 0.0) {
+        const u32 lim = (u32)(ceil(sc.thr * 4294967296.0) - 1.0);
+        const u32 any = elig[0] | elig[1];
+        u32 blocks = (any | (any >> 1)) & 0x55555555u, s0 = 0u, s1 = 0u;
+        while (blocks) {
+            const int y = __builtin_ctz(blocks);
+            blocks &= blocks - 1;
+            uint32_t r[4];
+            philox4x32(g.block(y), sc.gid, sc.step, tensor, sc.seed, r);
+            s0 |= ((r[0] <= lim ? 1u : 0u) | (r[2] <= lim ? 2u : 0u)) << y;
+            s1 |= ((r[1] <= lim ? 1u : 0u) | (r[3] <= lim ? 2u : 0u)) << y;
+        }
+        sp[0] = s0 & elig[0];
+        sp[1] = s1 & elig[1];
+    }
+}
+
+// Reference-order draws (stream_draws, sl_bits.h) per segment: ranks count the lower
+// lanes of the lane's own segment, the row prefix and the stream position are the
+// lane's env's own.
+__device__ __forceinline__ void seg_stream(const u32 elig[2], u32 sp[2], double thr,
+                                           const StreamSrc &src, int64_t pos, int lane) {
+    const uint64_t seg = 0xFFFFull << (16 * (lane >> 4));
+    const bool draw = thr > 0.0 && thr < 1.0;
+    const u32 rows = wave_or(elig[0] | elig[1]);
+    int pre = 0;
+    u32 s0 = 0u, s1 = 0u;
+#pragma unroll
+    for (int c = 0; c < 32; c += 4) {
+        if (((rows >> c) & 0xFu) == 0u) continue;
+        int64_t r[4][2];
+        bool e[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int y = c + k;
+            e[k][0] = (elig[0] >> y) & 1u;
+            e[k][1] = (elig[1] >> y) & 1u;
+            const uint64_t m0 = __ballot(e[k][0]) & seg, m1 = __ballot(e[k][1]) & seg;
+            const int64_t at = pos + pre + lanes_below(m0) + lanes_below(m1);
+            r[k][0] = at;
+            r[k][1] = at + (e[k][0] ? 1 : 0);
+            pre += __builtin_popcountll(m0) + __builtin_popcountll(m1);
+        }
+        double u[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int w = 0; w < 2; w++)
+                u[k][w] = (draw && e[k][w] && r[k][w] < src.n) ? src.draws[r[k][w]] : 1.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (draw && ((e[k][0] && r[k][0] >= src.n) || (e[k][1] && r[k][1] >= src.n)))
+                atomicOr((unsigned long long *)src.err, 1ull);
+            s0 |= ((e[k][0] && (thr >= 1.0 || u[k][0] < thr)) ? 1u : 0u) << (c + k);
+            s1 |= ((e[k][1] && (thr >= 1.0 || u[k][1] < thr)) ? 1u : 0u) << (c + k);
+        }
+    }
+    sp[0] = s0;
+    sp[1] = s1;
+}
+
+template <int MODE>
+struct GeoSeg {
+    int lane, j, H, W, nl;      // lane of the wave; j = lane within the env's segment
+    u32 mh;                     // the low H bits
+    int src_l, src_r;           // lanes holding columns 2j - 1 and 2j + 2
+    bool odd_last;              // word 1 is the column-0 copy (odd W)
+    StreamSrc src;
+    int64_t pos;
+    int count;
+    template <class F>
+    __device__ __forceinline__ V3 vert(const u32 *P, int w, F f) const {
+        const u32 x = f(P, w);
+        return V3{((x << 1) | (x >> (H - 1))) & mh, ((x >> 1) | ((x & 1u) << (H - 1))) & mh};
+    }
+    __device__ __forceinline__ H3 horiz(u32 w0, u32 w1) const {
+        const u32 right_col = odd_last ? w0 : w1;
+        return H3{(u32)__builtin_amdgcn_ds_bpermute(4 * src_l, (int)right_col),
+                  (u32)__builtin_amdgcn_ds_bpermute(4 * src_r, (int)w0)};
+    }
+    __device__ __forceinline__ bool halo_spawn() const { return false; }
+    __device__ __forceinline__ u32 block(int y) const { return (u32)((y >> 1) * nl + j); }
+    __device__ __forceinline__ void spawn(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
+                                          u32 tensor) {
+        const u32 e[2] = {elig[0], odd_last ? 0u : elig[1]};
+        if (MODE == SPAWN_PHILOX) {
+            seg_philox(*this, elig, sp, sc, tensor);
+        } else if (MODE == SPAWN_STREAM) {
+            seg_stream(e, sp, sc.thr, src, pos, lane);
+        } else {
+            count += __builtin_popcount(e[0]) + __builtin_popcount(e[1]);
+        }
+    }
+};
+
+// per-env record: field f of the lane's env (all lanes of the wave active)
+struct SegRecord {
+    u32 R[4];
+    int base;                    // byte address of the segment's lane 0 for ds_bpermute
+    __device__ __forceinline__ int get(int f) const {
+        return __builtin_amdgcn_ds_bpermute(base + 4 * (f & 15), (int)R[f >> 4]);
+    }
+};
+__device__ __forceinline__ SegRecord load_seg_record(const sl_env_state &st, const int32_t *actions,
+                                                     int64_t b, bool live, int lane) {
+    SegRecord r;
+    r.base = 4 * (lane & ~15);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        r.R[q] = live ? load_record(st, actions, b, 16 * q + (lane & 15)) : 0u;
+    return r;
+}
+
+// what epilogue_core reads, gathered while every lane is active (the epilogue then
+// runs on the segments' first lanes only); exits are already in the planes
+struct SegFields {
+    int op, ns, el, er, base, go, ax, ay, plen, phead, px, py, side;
+    double mp, bval;
+    __device__ int old_points() const { return op; }
+    __device__ int num_steps() const { return ns; }
+    __device__ int episode_length() const { return el; }
+    __device__ int episode_reward() const { return er; }
+    __device__ double min_performance() const { return mp; }
+    __device__ int baseline() const { return base; }
+    __device__ int exit_count() const { return 0; }
+    __device__ int exit_y(int) const { return 0; }
+    __device__ int exit_x(int) const { return 0; }
+    __device__ int game_over() const { return go; }
+    __device__ int agent_x() const { return ax; }
+    __device__ int agent_y() const { return ay; }
+    __device__ int prior_len() const { return plen; }
+    __device__ int prior_head() const { return phead; }
+    __device__ int prior_x(int) const { return px; }
+    __device__ int prior_y(int) const { return py; }
+    __device__ int side_effect() const { return side; }
+    __device__ double bonus(int) const { return bval; }
+};
+
+// Board, goals and start board of the wave's four envs into LDS by DMA: the four
+// envs are consecutive, so each tensor's part is one contiguous block of 4 * H * W
+// u16 in HBM (it starts 8-byte aligned: b0 is a multiple of 4), copied dword by dword
+// with global_load_lds (no registers held, every copy in flight at once).  Tensor t
+// sits at u16 offset t * kSegStride of the stage, env e's cell (y, x) at e * H * W +
+// y * W + x within it.
+constexpr int kSegStride = 4 * 32 * 32 + 128;       // u16 per staged tensor (4 envs,
+                                                     // 64-dword DMA granules)
+__device__ __forceinline__ void dma_seg(const sl_env_state &st, int64_t b0, int nenv,
+                                        lds_u32 *stage, int lane) {
+    const int64_t HW = (int64_t)st.H * st.W;
+    const int nbytes = (int)(nenv * HW * 2), nd = nbytes >> 2;
+    const uint16_t *src[3] = {st.board + b0 * HW, st.goals + b0 * HW, st.start_board + b0 * HW};
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+        const char *g = reinterpret_cast<const char *>(src[t]);
+        lds_u32 *dst = stage + t * (kSegStride / 2);
+        for (int k = 0; k * 64 < nd; k++) {
+            const int d = k * 64 + lane;
+            __builtin_amdgcn_global_load_lds((const void *)(g + 4 * (d < nd ? d : 0)),
+                                             (__attribute__((address_space(3))) void *)(dst + k * 64),
+                                             4, 0, 0);
+        }
+    }
+}
+// an odd cell count leaves each tensor's last u16 outside the dwords: copied after the
+// DMA has landed (its clamped lanes write the dwords past the block)
+__device__ __forceinline__ void dma_seg_tail(const sl_env_state &st, int64_t b0, int nenv,
+                                             lds_u32 *stage, int lane) {
+    const int64_t HW = (int64_t)st.H * st.W;
+    const int n = (int)(nenv * HW);
+    if ((n & 1) && lane < 3) {
+        const uint16_t *src = (lane == 0 ? st.board : lane == 1 ? st.goals : st.start_board) +
+                              b0 * HW;
+        reinterpret_cast<lds_u16 *>(stage + lane * (kSegStride / 2))[n - 1] = src[n - 1];
+    }
+}
+
+// the lane's dwords D[y] = cell(y, 2j) | cell(y, 2j + 1) << 16 of a staged tensor
+// (t: the env's cells; for odd W the last lane's second column is column 0)
+__device__ __forceinline__ void seg_rows(const lds_u16 *t, int H, int W, bool active, int j,
+                                         bool odd_last, u32 D[32]) {
+    const int x0 = 2 * j, x1 = odd_last ? 0 : 2 * j + 1;
+#pragma unroll
+    for (int y = 0; y < kMaxH; y++)
+        D[y] = (active && y < H) ? (u32)t[y * W + x0] | ((u32)t[y * W + x1] << 16) : 0u;
+}
+
+struct SegCells {       // unedited cells for the action (cell (y, x) at y * W + x)
+    const lds_u16 *cells;
+    __device__ __forceinline__ uint32_t operator()(int i) const { return cells[i]; }
+};
+
+// 2 waves/SIMD is the register budget: a 4096-env batch is 1024 waves, one per SIMD
+template <int MODE>
+__global__ void __launch_bounds__(64, 2)
+k_env_step_seg4(SmallKArgs ka) {
+    const sl_env_state &st = ka.st;
+    const StepArgs &a = ka.a;
+    const int lane = threadIdx.x, e = lane >> 4, j = lane & 15;
+    const int64_t b0 = 4 * (int64_t)blockIdx.x;
+    const int nenv = (int)min((int64_t)4, st.B - b0);
+    const int64_t b = b0 + e;
+    const bool live = e < nenv;                       // this segment holds an env
+    const int H = st.H, W = st.W, nl = (W + 1) >> 1;
+    const bool active = live && j < nl;
+    extern __shared__ __attribute__((aligned(16))) u32 dyn_stage[];
+    lds_u16 *stage = (lds_u16 *)dyn_stage;
+    const int env_off = e * H * W;
+    lds_u16 *sb = stage + env_off, *sg = sb + kSegStride, *ss = sg + kSegStride;
+
+    GeoSeg<MODE> geo;
+    geo.lane = lane;
+    geo.j = j;
+    geo.H = H;
+    geo.W = W;
+    geo.nl = nl;
+    geo.mh = H == 32 ? ~0u : ((1u << H) - 1u);
+    geo.src_l = (lane & ~15) + (active ? (j == 0 ? nl - 1 : j - 1) : j);
+    geo.src_r = (lane & ~15) + (active ? (j + 1 == nl ? 0 : j + 1) : j);
+    geo.odd_last = (W & 1) && j == nl - 1;
+    geo.src = StreamSrc{a.draws, a.n_draws, nullptr};
+    geo.count = 0;
+    const u32 wm0 = active ? geo.mh : 0u, wm1 = (active && !geo.odd_last) ? geo.mh : 0u;
+    int64_t pos_b = 0, pos_g = 0;
+    if (MODE == SPAWN_STREAM && live) {
+        const Scratch w = scratch_of(ka.scratch, st.B);
+        geo.src.err = w.err;
+        pos_b = w.offsets[2 * b];
+        pos_g = w.offsets[2 * b + 1];
+    }
+
+    dma_seg(st, b0, nenv, (lds_u32 *)dyn_stage, lane);
+    const SegRecord rc = load_seg_record(st, ka.actions, live ? b : b0, live, lane);
+    wait_vm();
+    dma_seg_tail(st, b0, nenv, (lds_u32 *)dyn_stage, lane);
+    wait_lgkm();
+    u32 PB[32], PG[32];
+    seg_rows(sg, H, W, active, j, geo.odd_last, PG);
+
+    SpawnCtx sc;
+    sc.gid = a.env0 + (uint32_t)b;
+    sc.step = a.step;
+    sc.seed = a.seed;
+    sc.thr = (double)__int_as_float(rc.get(R_SPAWN));
+
+    // ---- goals: rule, then store the changed rows
+    transpose32(PG);
+    u32 cg[2];
+    geo.pos = pos_g;
+    rule_planes(PG, cg, geo, sc, 1u);
+    cg[0] &= wm0;
+    cg[1] &= wm1;
+    const u32 rg = seg_or(cg[0] | cg[1]);
+    u32 gcol[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        gcol[k][0] = PL(PG, 9 + k, 0) & wm0;
+        gcol[k][1] = PL(PG, 9 + k, 1) & wm1;
+    }
+    const int64_t off = b * (int64_t)H * W;
+    const int c0 = 2 * j, c1 = 2 * j + 1;
+    if (__ballot(rg != 0u)) {
+        transpose32(PG);
+        uint16_t *gg = st.goals + off;
+#pragma unroll
+        for (int y = 0; y < kMaxH; y++)
+            if (((rg >> y) & 1u) && active) {
+                gg[y * W + c0] = (uint16_t)PG[y];
+                if (!geo.odd_last) gg[y * W + c1] = (uint16_t)(PG[y] >> 16);
+            }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- the action: each segment's first lane, on its staged board (edits go
+    // straight into the stage, the column-0 copy of an odd board too)
+    const int go0 = rc.get(R_GO), ax0 = rc.get(R_AX), ay0 = rc.get(R_AY);
+    RecEnv env{st, b, go0, ax0, ay0, rc.get(R_SCORE), rc.get(R_BASE), rc.get(R_POSS),
+               __hiloint2double(rc.get(R_MP + 1), rc.get(R_MP))};
+    SegFields fl;
+    fl.op = rc.get(R_OLDP);
+    fl.ns = rc.get(R_NSTEPS);
+    fl.el = rc.get(R_EPLEN);
+    fl.er = rc.get(R_EPREW);
+    fl.base = env.base;
+    fl.mp = env.mp;
+    fl.plen = rc.get(R_PLEN);
+    fl.phead = rc.get(R_PHEAD);
+    fl.side = rc.get(R_SIDE);
+    const int act = rc.get(R_ACT);
+    const int phead = min(max(fl.phead, 0), 15);
+    // the prior ring entry at the head, by a second bpermute with a per-lane field
+    const int pxh = __builtin_amdgcn_ds_bpermute(rc.base + 4 * phead, (int)rc.R[R_PX >> 4]);
+    const int pyh = __builtin_amdgcn_ds_bpermute(rc.base + 4 * phead, (int)rc.R[R_PY >> 4]);
+    int act_reward = 0;
+    u32 erow = 0;
+    if (MODE == SPAWN_STREAM) {
+        act_reward = live ? (int)scratch_of(ka.scratch, st.B).act[b] : 0;
+    } else if (j == 0 && live) {
+        OverlayT<SegCells> ov;
+        ov.src.cells = sb;
+        ov.n = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            ov.idx[k] = 0;
+            ov.val[k] = 0;
+        }
+        act_reward = act_core(env, act, H, W, ka.ctp, ka.ctc, ov);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k < ov.n) {
+                const int i = ov.idx[k];
+                sb[i] = (uint16_t)ov.val[k];
+                erow |= 1u << (i / W);
+            }
+    }
+    // the post-action agent and game-over flag, and the edited rows, to the segment
+    const int sl0 = (lane & ~15) * 4;
+    fl.go = __builtin_amdgcn_ds_bpermute(sl0, env.go);
+    fl.ax = __builtin_amdgcn_ds_bpermute(sl0, env.ax);
+    fl.ay = __builtin_amdgcn_ds_bpermute(sl0, env.ay);
+    act_reward = __builtin_amdgcn_ds_bpermute(sl0, act_reward);
+    erow = (u32)__builtin_amdgcn_ds_bpermute(sl0, (int)erow);
+    fl.px = pxh;
+    fl.py = pyh;
+    fl.bval = 0.0;
+    if (a.bonus_period > 0 && live)
+        fl.bval = a.bonus_table[bonus_dist(fl.ax, fl.ay, fl.px, fl.py, fl.plen, a.bonus_period,
+                                           a.bonus_len)];
+    seg_rows(sb, H, W, active, j, geo.odd_last, PB);
+    transpose32(PB);
+    const u32 old9[2] = {PL(PB, 9, 0), PL(PB, 9, 1)};
+    u32 cb[2];
+    geo.pos = pos_b;
+    rule_planes(PB, cb, geo, sc, 0u);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- scores over the real cells of the new board and goals
+    u32 PS[32];
+    seg_rows(ss, H, W, active, j, geo.odd_last, PS);
+    transpose32(PS);
+#pragma unroll
+    for (int p = 0; p < 16; p++) {
+        PL(PB, p, 0) &= wm0;
+        PL(PB, p, 1) &= wm1;
+        PL(PS, p, 0) &= wm0;
+        PL(PS, p, 1) &= wm1;
+    }
+    int pts, scr, pos, side;
+    score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
+    const int s1 = seg_total((pts + 192) | ((scr + 64) << 16));
+    const int s2 = seg_total(pos | (side << 16));
+    const int points = (s1 & 0xFFFF) - 192 * 16;
+    const int score = ((s1 >> 16) & 0xFFFF) - 64 * 16;
+    const int possible = s2 & 0xFFFF;
+    const int side_total = (s2 >> 16) & 0xFFFF;
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- exits coloured in the planes (update_exit_colors); the rows whose cells
+    // changed -- by the rule, the action or an exit's colour -- are stored
+    const bool can = can_exit_now(fl.mp, score, fl.base, possible);
+    u32 ch = (cb[0] & wm0) | (cb[1] & wm1);
+#pragma unroll
+    for (int w = 0; w < 2; w++) {
+        const u32 n9 = can ? (PL(PB, 9, w) | PL(PB, 8, w)) : (PL(PB, 9, w) & ~PL(PB, 8, w));
+        ch |= (n9 ^ (PL(PB, 8, w) & (w ? old9[1] : old9[0]))) & PL(PB, 8, w) & (w ? wm1 : wm0);
+        PL(PB, 9, w) = n9;
+    }
+    const u32 rb = seg_or(ch) | erow;
+    if (__ballot(rb != 0u)) {
+        transpose32(PB);
+        uint16_t *gb = st.board + off;
+#pragma unroll
+        for (int y = 0; y < kMaxH; y++)
+            if (((rb >> y) & 1u) && active) {
+                gb[y * W + c0] = (uint16_t)PB[y];
+                if (!geo.odd_last) gb[y * W + c1] = (uint16_t)(PB[y] >> 16);
+            }
+    }
+    int rs = 0;
+    if (j == 0 && live) {
+        const SmallKArgs &k = kargs();
+        rs = epilogue_core(k.st, k.a, b, fl, act_reward, points, score, possible, side_total,
+                           k.reward_out, k.done_out, k.flags_out, k.ep_len_out, k.ep_rew_out)
+                 ? 1 : 0;
+    }
+    uint64_t resets = __ballot(rs != 0);
+    if (resets) {
+        const SmallKArgs &k = kargs();
+        if (k.pool.K > 0) {
+            wait_vm();         // this step's stores to the envs have completed
+            while (resets) {
+                const int l = __builtin_ctzll(resets);
+                resets &= resets - 1;
+                small_reset(k.st, k.pool, k.ra, b0 + (l >> 4), lane);
+            }
+        }
+    }
+}
+
 // Replay-mode prologue of env b (SL_RNG_STREAM), one wave: the action (state, its
 // cell edits into the board in HBM, its reward into scratch act[b]), then the eligible
 // cells of the acted-on board and of the goals (scratch counts[2b], [2b+1];
@@ -522,16 +961,26 @@ int launch_step_small(const sl_env_state &st, const StepArgs &a, const FastExtra
                         fx.ra, fx.scratch};
     const size_t lds = (size_t)3 * st.H * 32 * sizeof(uint32_t);
     const dim3 grid((unsigned)st.B);
+    // boards up to 32 wide: four envs per wave
+    const bool seg = st.W <= kSegW;
+    const dim3 grid4((unsigned)((st.B + 3) / 4));
+    const size_t lds4 = (size_t)3 * kSegStride * sizeof(uint16_t);
     if (fx.stream) {
         hipLaunchKernelGGL(k_stream_prologue_small, grid, dim3(64), lds, s, ka);
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
         const int rc = stream_offsets(st, fx, s);
         if (rc) return rc;
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        hipLaunchKernelGGL(k_env_step_small<SPAWN_STREAM>, grid, dim3(64), lds, s, ka);
+        if (seg)
+            hipLaunchKernelGGL(k_env_step_seg4<SPAWN_STREAM>, grid4, dim3(64), lds4, s, ka);
+        else
+            hipLaunchKernelGGL(k_env_step_small<SPAWN_STREAM>, grid, dim3(64), lds, s, ka);
     } else {
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        hipLaunchKernelGGL(k_env_step_small<SPAWN_PHILOX>, grid, dim3(64), lds, s, ka);
+        if (seg)
+            hipLaunchKernelGGL(k_env_step_seg4<SPAWN_PHILOX>, grid4, dim3(64), lds4, s, ka);
+        else
+            hipLaunchKernelGGL(k_env_step_small<SPAWN_PHILOX>, grid, dim3(64), lds, s, ka);
     }
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }

@@ -489,11 +489,12 @@ def _synthetic_pool(rng, K, H, W):
 
 
 @pytest.mark.parametrize("shape", [(25, 25), (26, 26), (2, 2), (3, 5), (32, 63), (17, 64),
-                                   (31, 2)])
+                                   (31, 2), (9, 31), (32, 32), (25, 33)])
 def test_small_kernel_vs_generic(torch_dev, shape):
-    """Boards up to 32x64 take the bit-sliced small kernel (column pairs over all rows,
-    ds_bpermute wrap at W, odd W via a column-0 copy): bit-exact with the generic
-    kernel through actions, spawns, exits and resets."""
+    """Boards up to 32x64 take the bit-sliced small kernels (column pairs over all rows,
+    ds_bpermute wrap at W, odd W via a column-0 copy; up to 32 wide four envs share a
+    wave, and batches that are no multiple of 4 leave segments empty): bit-exact with
+    the generic kernel through actions, spawns, exits and resets."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
     H, W = shape
@@ -503,7 +504,7 @@ def test_small_kernel_vs_generic(torch_dev, shape):
                                spawn_frac=0.01)
     else:
         pool = _synthetic_pool(rng, 8, H, W)
-    B, T = 96, 70
+    B, T = 94 + (H + W) % 4, 70
     kw = dict(time_limit=23, view_shape=(9, 9), output_channels=None, penalty_coef=0.7,
               min_performance=0.01, rng="philox", seed=5, level_order="random",
               augment_roll=True)
