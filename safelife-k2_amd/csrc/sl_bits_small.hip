@@ -544,12 +544,18 @@ __device__ __forceinline__ void seg_stream(const u32 elig[2], u32 sp[2], double 
     sp[1] = s1;
 }
 
-template <int MODE>
+// DPPN: the neighbouring column pairs come from DPP row rotations (row_ror:1 / :15,
+// no LDS round trip): a segment's spare lanes hold copies so that the rotations wrap
+// at nl -- lane nl a copy of lane 0 (the right neighbour of lane nl - 1) and lane 15
+// a copy of lane nl - 1 (the left neighbour of lane 0); nl = 16 wraps by itself.  For
+// nl = 15 one spare lane cannot be both, and ds_bpermute is used instead.
+template <int MODE, bool DPPN>
 struct GeoSeg {
     int lane, j, H, W, nl;      // lane of the wave; j = lane within the env's segment
     u32 mh;                     // the low H bits
-    int src_l, src_r;           // lanes holding columns 2j - 1 and 2j + 2
+    int src_l, src_r;           // lanes holding columns 2j - 1 and 2j + 2 (ds_bpermute)
     bool odd_last;              // word 1 is the column-0 copy (odd W)
+    bool real;                  // the lane holds its own column pair (not a copy)
     StreamSrc src;
     int64_t pos;
     int count;
@@ -560,16 +566,19 @@ struct GeoSeg {
     }
     __device__ __forceinline__ H3 horiz(u32 w0, u32 w1) const {
         const u32 right_col = odd_last ? w0 : w1;
+        if (DPPN) return H3{dpp<0x121>(right_col), dpp<0x12F>(w0)};    // row_ror:1, :15
         return H3{(u32)__builtin_amdgcn_ds_bpermute(4 * src_l, (int)right_col),
                   (u32)__builtin_amdgcn_ds_bpermute(4 * src_r, (int)w0)};
     }
     __device__ __forceinline__ bool halo_spawn() const { return false; }
     __device__ __forceinline__ u32 block(int y) const { return (u32)((y >> 1) * nl + j); }
+    // copies and the column-0 copy draw nothing (their results are discarded, and in
+    // replay mode they must not shift the real cells' ranks)
     __device__ __forceinline__ void spawn(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
                                           u32 tensor) {
-        const u32 e[2] = {elig[0], odd_last ? 0u : elig[1]};
+        const u32 e[2] = {real ? elig[0] : 0u, (real && !odd_last) ? elig[1] : 0u};
         if (MODE == SPAWN_PHILOX) {
-            seg_philox(*this, elig, sp, sc, tensor);
+            seg_philox(*this, e, sp, sc, tensor);
         } else if (MODE == SPAWN_STREAM) {
             seg_stream(e, sp, sc.thr, src, pos, lane);
         } else {
@@ -675,7 +684,7 @@ struct SegCells {       // unedited cells for the action (cell (y, x) at y * W +
 };
 
 // 2 waves/SIMD is the register budget: a 4096-env batch is 1024 waves, one per SIMD
-template <int MODE>
+template <int MODE, bool DPPN>
 __global__ void __launch_bounds__(64, 2)
 k_env_step_seg4(SmallKArgs ka) {
     const sl_env_state &st = ka.st;
@@ -692,7 +701,10 @@ k_env_step_seg4(SmallKArgs ka) {
     const int env_off = e * H * W;
     lds_u16 *sb = stage + env_off, *sg = sb + kSegStride, *ss = sg + kSegStride;
 
-    GeoSeg<MODE> geo;
+    // the column pair this lane holds: its own, or (DPPN) the copy a rotation needs
+    const int js = j < nl ? j : (DPPN ? (j == 15 ? nl - 1 : (j == nl ? 0 : -1)) : -1);
+    const bool holds = live && js >= 0;
+    GeoSeg<MODE, DPPN> geo;
     geo.lane = lane;
     geo.j = j;
     geo.H = H;
@@ -701,7 +713,8 @@ k_env_step_seg4(SmallKArgs ka) {
     geo.mh = H == 32 ? ~0u : ((1u << H) - 1u);
     geo.src_l = (lane & ~15) + (active ? (j == 0 ? nl - 1 : j - 1) : j);
     geo.src_r = (lane & ~15) + (active ? (j + 1 == nl ? 0 : j + 1) : j);
-    geo.odd_last = (W & 1) && j == nl - 1;
+    geo.odd_last = (W & 1) && js == nl - 1;
+    geo.real = active;
     geo.src = StreamSrc{a.draws, a.n_draws, nullptr};
     geo.count = 0;
     const u32 wm0 = active ? geo.mh : 0u, wm1 = (active && !geo.odd_last) ? geo.mh : 0u;
@@ -719,7 +732,7 @@ k_env_step_seg4(SmallKArgs ka) {
     dma_seg_tail(st, b0, nenv, (lds_u32 *)dyn_stage, lane);
     wait_lgkm();
     u32 PB[32], PG[32];
-    seg_rows(sg, H, W, active, j, geo.odd_last, PG);
+    seg_rows(sg, H, W, holds, js, geo.odd_last, PG);
 
     SpawnCtx sc;
     sc.gid = a.env0 + (uint32_t)b;
@@ -810,7 +823,7 @@ k_env_step_seg4(SmallKArgs ka) {
     if (a.bonus_period > 0 && live)
         fl.bval = a.bonus_table[bonus_dist(fl.ax, fl.ay, fl.px, fl.py, fl.plen, a.bonus_period,
                                            a.bonus_len)];
-    seg_rows(sb, H, W, active, j, geo.odd_last, PB);
+    seg_rows(sb, H, W, holds, js, geo.odd_last, PB);
     transpose32(PB);
     const u32 old9[2] = {PL(PB, 9, 0), PL(PB, 9, 1)};
     u32 cb[2];
@@ -820,7 +833,7 @@ k_env_step_seg4(SmallKArgs ka) {
 
     // ---- scores over the real cells of the new board and goals
     u32 PS[32];
-    seg_rows(ss, H, W, active, j, geo.odd_last, PS);
+    seg_rows(ss, H, W, holds, js, geo.odd_last, PS);
     transpose32(PS);
 #pragma unroll
     for (int p = 0; p < 16; p++) {
@@ -963,6 +976,7 @@ int launch_step_small(const sl_env_state &st, const StepArgs &a, const FastExtra
     const dim3 grid((unsigned)st.B);
     // boards up to 32 wide: four envs per wave
     const bool seg = st.W <= kSegW;
+    const bool dppn = (st.W + 1) / 2 != 15;      // GeoSeg: DPP neighbours unless nl = 15
     const dim3 grid4((unsigned)((st.B + 3) / 4));
     const size_t lds4 = (size_t)3 * kSegStride * sizeof(uint16_t);
     if (fx.stream) {
@@ -971,14 +985,18 @@ int launch_step_small(const sl_env_state &st, const StepArgs &a, const FastExtra
         const int rc = stream_offsets(st, fx, s);
         if (rc) return rc;
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        if (seg)
-            hipLaunchKernelGGL(k_env_step_seg4<SPAWN_STREAM>, grid4, dim3(64), lds4, s, ka);
+        if (seg && dppn)
+            hipLaunchKernelGGL((k_env_step_seg4<SPAWN_STREAM, true>), grid4, dim3(64), lds4, s, ka);
+        else if (seg)
+            hipLaunchKernelGGL((k_env_step_seg4<SPAWN_STREAM, false>), grid4, dim3(64), lds4, s, ka);
         else
             hipLaunchKernelGGL(k_env_step_small<SPAWN_STREAM>, grid, dim3(64), lds, s, ka);
     } else {
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        if (seg)
-            hipLaunchKernelGGL(k_env_step_seg4<SPAWN_PHILOX>, grid4, dim3(64), lds4, s, ka);
+        if (seg && dppn)
+            hipLaunchKernelGGL((k_env_step_seg4<SPAWN_PHILOX, true>), grid4, dim3(64), lds4, s, ka);
+        else if (seg)
+            hipLaunchKernelGGL((k_env_step_seg4<SPAWN_PHILOX, false>), grid4, dim3(64), lds4, s, ka);
         else
             hipLaunchKernelGGL(k_env_step_small<SPAWN_PHILOX>, grid, dim3(64), lds, s, ka);
     }

@@ -41,7 +41,8 @@ def test_labels():
     assert "25×25" in bench.metric_name(25, 25, 4096)
     assert bench.step_kernel_name(64, 64, "none", "auto") == "k_env_step_bits64<false, 0>"
     assert bench.step_kernel_name(64, 64, "packed", "auto") == "k_env_step_bits64<true, 0>"
-    assert bench.step_kernel_name(25, 25, "none", "auto") == "k_env_step_seg4<0>"
+    assert bench.step_kernel_name(25, 25, "none", "auto") == "k_env_step_seg4<0, true>"
+    assert bench.step_kernel_name(25, 29, "none", "auto") == "k_env_step_seg4<0, false>"
     assert bench.step_kernel_name(25, 40, "none", "auto") == "k_env_step_small<0>"
     assert bench.step_kernel_name(128, 128, "none", "auto") == "k_env_step_bits128<0>"
     assert (bench.step_kernel_name(128, 128, "none", "auto", "stream")

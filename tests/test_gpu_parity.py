@@ -489,7 +489,7 @@ def _synthetic_pool(rng, K, H, W):
 
 
 @pytest.mark.parametrize("shape", [(25, 25), (26, 26), (2, 2), (3, 5), (32, 63), (17, 64),
-                                   (31, 2), (9, 31), (32, 32), (25, 33)])
+                                   (31, 2), (9, 31), (32, 32), (25, 33), (7, 29), (20, 28)])
 def test_small_kernel_vs_generic(torch_dev, shape):
     """Boards up to 32x64 take the bit-sliced small kernels (column pairs over all rows,
     ds_bpermute wrap at W, odd W via a column-0 copy; up to 32 wide four envs share a
