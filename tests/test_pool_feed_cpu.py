@@ -60,3 +60,20 @@ def test_levels_archive(tmp_path):
     lv = list(npz_level_source(str(tmp_path / "archive.npz"), repeat=False))
     assert len(lv) == 3 and np.array_equal(lv[2]["goals"], d["goals"][2])
     assert LevelPool.from_levels(lv).K == 3
+
+
+def test_level_pool_exit_cap():
+    """Documented divergence: the device state keeps at most SL_MAX_EXITS exit cells
+    per env (their positions for the observation and the exit recolouring); levels
+    with more are rejected when the pool is built, not silently truncated (the
+    reference's update_exit_colors, safelife_game.py:528-537, has no cap)."""
+    from safelife_amd import _lib
+    K, H, W = 1, 16, 16
+    board = np.zeros((K, H, W), np.uint16)
+    goals = np.zeros_like(board)
+    ys, xs = np.divmod(np.arange(_lib.SL_MAX_EXITS) * 3 + 20, W)
+    board[0, ys, xs] = 272                                  # level exits
+    LevelPool(board, goals, [(0, 0)], [0], [0.3], [0.01])   # at the cap: accepted
+    board[0, 15, 15] = 272
+    with pytest.raises(ValueError, match="exits"):
+        LevelPool(board, goals, [(0, 0)], [0], [0.3], [0.01])
