@@ -52,11 +52,14 @@ extern "C" {
 #define SL_ETOOBIG (-3)     /* board too large for the selected kernel */
 
 #define SL_RNG_STREAM 0     /* replay a supplied uniform stream (reference order) */
-#define SL_RNG_PHILOX 1     /* counter-based Philox4x32-10 (production) */
+#define SL_RNG_PHILOX 1     /* counter-based Philox4x32-10 (production): the four
+                               cells of a 2x2 block share one evaluation,
+                               counter (block, env, step, tensor), 32-bit words */
 
 #define SL_KERNEL_AUTO 0     /* bit-sliced kernels for 64x64, 128x128 and boards
-                                up to 32x64 in Philox mode, the generic kernel
-                                otherwise                                    */
+                                up to 32x64 (both RNG modes; replay adds a
+                                prologue kernel + a scan per step), the generic
+                                kernel for other shapes                      */
 #define SL_KERNEL_GENERIC 1  /* LDS-staged per-cell kernel, any shape        */
 #define SL_KERNEL_FAST 2     /* require the fast kernel (error if none)      */
 
@@ -275,7 +278,8 @@ typedef struct sl_env_cfg {
     int64_t n_draws;
     int64_t *stream_pos;            /* dev [1]: next unread draw (advanced)    */
     int64_t *scratch;               /* dev [8*B + 16] workspace, zeroed once
-                                     * before the first step.  With auto_reset the
+                                     * before the first step (layout:
+                                     * sl_env_common.h Scratch).  With auto_reset the
                                      * 64x64 / 128x128 kernels queue finished envs
                                      * in per-parity lists (words 8B+2, 8B+3) that
                                      * stay valid only over consecutive steps
@@ -287,8 +291,10 @@ typedef struct sl_env_cfg {
                                        1: Philox-random level                  */
     int32_t n_total_envs;           /* envs across all shards                  */
     int32_t augment_roll;           /* 1: random toroidal roll per episode     */
-    void *ev_begin, *ev_end;        /* optional hipEvent_t pair recorded around
-                                       the board-advance kernel (profiling)    */
+    void *ev_begin, *ev_end;        /* optional hipEvent_t pair recorded right
+                                       before and after the board-advance (step)
+                                       kernel's launch (profiling; an event record
+                                       holds the next dispatch until written)  */
     int32_t kernel;                 /* SL_KERNEL_*: which advance kernel       */
     void *obs_out;                  /* dev: sl_env_step also writes every env's
                                        observation after the step (auto-resets

@@ -224,9 +224,12 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
             D[y] = (u32)lv[sr + c0] | ((u32)lv[sr + c1] << 16);
         }
     };
-    // goals: copy, then keep their colour planes for the sums
-    u32 P[32];
+    // both gathers in flight together; the board's rows serve the start board (as
+    // loaded), the sums (transposed copy) and the board itself (exits coloured)
+    u32 P[32], D[32];
     rolled(lg, P);
+    rolled(lb, D);
+    // goals: copy, then keep their colour planes for the sums
 #pragma unroll
     for (int y = 0; y < 32; y++) gg[y * 32] = P[y];
     transpose32(P);
@@ -243,9 +246,11 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
     }
     const bool sg = __ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull;
     // start board: copy, then the sums over the initial board and goals
-    rolled(lb, P);
 #pragma unroll
-    for (int y = 0; y < 32; y++) gs[y * 32] = P[y];
+    for (int y = 0; y < 32; y++) {
+        gs[y * 32] = D[y];
+        P[y] = D[y];
+    }
     transpose32(P);
     int pts, scr, pos, side;
     score_planes(P, gcol, P, &pts, &scr, &pos, &side);
@@ -260,8 +265,6 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
     const u32 ex0 = PL(P, 8, 0), ex1 = PL(P, 8, 1);       // exit planes
     // the board: the start board with its exits coloured (update_exit_colors)
     {
-        u32 D[32];
-        rolled(lb, D);
 #pragma unroll
         for (int y = 0; y < 32; y++) {
             u32 d = D[y];
