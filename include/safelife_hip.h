@@ -191,9 +191,13 @@ typedef struct sl_env_state {
     int32_t *level_index;     /* level of the current episode                 */
     int32_t *episodes;        /* episodes started by this env                 */
     int32_t *num_steps;       /* game.num_steps                               */
-    int32_t *spawn_flags;     /* bit0: board, bit1: goals hold a spawning cell
-                                 (set at reset; spawning bits are never created
-                                 by the rule or the actions, only moved)       */
+    int32_t *spawn_flags;     /* bit0: board, bit1: goals may hold a spawning
+                                 cell (set at reset; spawning bits are never
+                                 created by the rule or the actions -- except a
+                                 power toggle, which the kernels allow for -- only
+                                 moved).  The replay prologues skip the eligible
+                                 count of a tensor whose bit is clear: a caller
+                                 writing state sets both bits.                 */
     int32_t *start_roll;      /* (dy << 16) | dx: start_board[b] equals pool
                                  level level_index[b] rolled by (dy, dx) (set by
                                  every reset); -1: start_board was written by

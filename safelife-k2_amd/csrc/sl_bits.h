@@ -472,6 +472,7 @@ enum : int {
     R_MP = 19,           // min_performance, 2 dwords
     R_EY = 21,           // exit_y[8] (int16), 4 dwords
     R_EX = 25,           // exit_x[8], 4 dwords
+    R_SPF = 29,          // spawn_flags: bit0 the board, bit1 the goals may hold a spawner
     R_PX = 32,           // prior_x[16]
     R_PY = 48            // prior_y[16]
 };
@@ -500,6 +501,7 @@ __device__ __forceinline__ u32 load_record(const sl_env_state &st, const int32_t
     SL_SEL(R_PHEAD, st.prior_head);
     SL_SEL(R_SIDE, st.side_effect);
     SL_SEL(R_POK, st.planes_ok);
+    SL_SEL(R_SPF, st.spawn_flags);
 #undef SL_SEL
     if (lane >= R_MP && lane < R_MP + 2) {
         p = reinterpret_cast<const char *>(st.min_performance);

@@ -681,7 +681,7 @@ k_env_step_bits64(StepKArgs ka) {
 // Replay-mode prologue of env b (SL_RNG_STREAM), one wave: the action (state, its
 // cell edits into the board in HBM, its reward into scratch act[b]), then the eligible
 // cells -- the uniforms the step will draw -- of the acted-on board and of the goals
-// (scratch counts[2b], [2b+1]; k_scan_i64 turns them into each tensor's first
+// (scratch counts[2b], [2b+1]; sl_exclusive_scan_i64 turns them into each tensor's first
 // uniform).  The work of k_env_action + k_env_count (sl_env.hip) on the bit-sliced rule.
 __global__ void __launch_bounds__(64)
 k_stream_prologue64(StepKArgs ka) {
@@ -691,8 +691,11 @@ k_stream_prologue64(StepKArgs ka) {
     const int64_t off = b * (int64_t)(N * N);
     const int lane_off = (lane & 1) * 1024 + (lane >> 1);
     const u32 V = load_record(st, ka.actions, b, lane);
+    // a board or goals without spawners (spawn_flags, set at reset: no rule or action
+    // creates one) draws nothing: its count is 0 without a read
+    const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);     // toggling powers can make one
     u32 P[32];
-    load_pairs<32>(reinterpret_cast<const u32 *>(st.board + off) + lane_off, P);
+    if (spf & 1) load_pairs<32>(reinterpret_cast<const u32 *>(st.board + off) + lane_off, P);
     OverlayT<GlobalCells> ov;
     ov.src.bd = st.board + off;
     ov.n = 0;
@@ -719,16 +722,19 @@ k_stream_prologue64(StepKArgs ka) {
         eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
     }
     SpawnCtx sc{0u, 0u, 0ull, 0.0};
-    transpose32(P);
-    (void)mux_edits(P, ne, eidx, eval, lane);
     u32 ch[2];
-    Geo64<SPAWN_COUNT> gbd{lane, StreamSrc{nullptr, 0, nullptr}, 0, 0};
-    rule_planes(P, ch, gbd, sc, 0u);
-    const int nb = wave_total(gbd.count);
+    int nb = 0;
+    if (spf & 1) {
+        transpose32(P);
+        (void)mux_edits(P, ne, eidx, eval, lane);
+        Geo64<SPAWN_COUNT> gbd{lane, StreamSrc{nullptr, 0, nullptr}, 0, 0};
+        rule_planes(P, ch, gbd, sc, 0u);
+        nb = wave_total(gbd.count);
+    }
     // goals at their fixed point (planes_ok bit 2) hold no spawner: no draws
     const int pok = (st.planes && st.planes_ok) ? rec(V, R_POK) & 6 : 0;
     int ng = 0;
-    if ((pok & 6) != 6) {
+    if ((pok & 6) != 6 && (spf & 2)) {
         if (pok & 2) {
             const u32 *mg = st.planes + b * 4096 + 2048 + lane;
 #pragma unroll

@@ -372,7 +372,7 @@ k_env_step_bits128(Step128KArgs ka) {
 // Replay-mode prologue of env b (SL_RNG_STREAM), one wave: the action (state, its
 // cell edits into the board in HBM, its reward into scratch act[b]), then the eligible
 // cells of the acted-on board and of the goals, band by band (scratch counts[2b],
-// [2b+1]; k_scan_i64 turns them into each tensor's first uniform).  The work of
+// [2b+1]; sl_exclusive_scan_i64 turns them into each tensor's first uniform).  The work of
 // k_env_action + k_env_count (sl_env.hip) on the bit-sliced rule.
 __global__ void __launch_bounds__(64)
 k_stream_prologue128(Step128KArgs ka) {
@@ -432,9 +432,11 @@ k_stream_prologue128(Step128KArgs ka) {
         }
         return wave_total(n);
     };
-    const int nb = count(gb, true);
-    // goals at their fixed point (planes_ok bit 2) hold no spawner: no draws
-    const int ng = (rec(V, R_POK) & 6) == 6 ? 0 : count(gg, false);
+    // a board or goals without spawners (spawn_flags, set at reset: no rule or action
+    // creates one) draws nothing; nor do goals at their fixed point (planes_ok bit 2)
+    const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);     // toggling powers can make one
+    const int nb = (spf & 1) ? count(gb, true) : 0;
+    const int ng = ((rec(V, R_POK) & 6) == 6 || !(spf & 2)) ? 0 : count(gg, false);
     if (lane == 0) {
         w.counts[2 * b] = nb;
         w.counts[2 * b + 1] = ng;

@@ -897,7 +897,7 @@ k_env_step_seg4(SmallKArgs ka) {
 // Replay-mode prologue of env b (SL_RNG_STREAM), one wave: the action (state, its
 // cell edits into the board in HBM, its reward into scratch act[b]), then the eligible
 // cells of the acted-on board and of the goals (scratch counts[2b], [2b+1];
-// k_scan_i64 turns them into each tensor's first uniform).  The work of k_env_action
+// sl_exclusive_scan_i64 turns them into each tensor's first uniform).  The work of k_env_action
 // + k_env_count (sl_env.hip) on the bit-sliced rule.
 __global__ void __launch_bounds__(64)
 k_stream_prologue_small(SmallKArgs ka) {
@@ -938,9 +938,13 @@ k_stream_prologue_small(SmallKArgs ka) {
         }
     }
     SpawnCtx sc{0u, 0u, 0ull, 0.0};
-    int n[2];
+    int n[2] = {0, 0};
+    // no spawner in the tensor (spawn_flags, set at reset; toggling powers can make
+    // one on the board): no draws
+    const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);
 #pragma unroll 1
     for (int t = 0; t < 2; t++) {
+        if (!((spf >> t) & 1)) continue;
         u32 P[32];
         lds_rows((const lds_u16 *)stage[t], H, active, lane, P);
         transpose32(P);

@@ -2,7 +2,7 @@
 //
 //   sl_advance          speedups.advance_board over B boards (module.c:19-44)
 //   sl_count_eligible   draws one advance consumes (advance_board.c:110)
-//   sl_exclusive_scan_i64
+//   sl_exclusive_scan_i64      three-launch chunked scan (k_scan_reduce / _chunks / _apply)
 //   sl_side_effect_densities   the rollout + density half of side_effect_score
 //                              (side_effects.py:59-92,131-139), batched over episodes
 //
@@ -124,30 +124,84 @@ k_count_eligible(const uint16_t *__restrict__ in, int64_t *__restrict__ counts, 
 }
 
 // single-workgroup exclusive scan (parity / replay path only: n <= a few 1e5)
-__global__ void __launch_bounds__(1024)
-k_scan_i64(const int64_t *__restrict__ in, int64_t *__restrict__ out, int64_t n,
-           const int64_t *__restrict__ base, int64_t *__restrict__ total_out) {
-    __shared__ int64_t part[1024];
-    __shared__ int64_t carry;
-    if (threadIdx.x == 0) carry = base ? base[0] : 0;
-    __syncthreads();
-    for (int64_t s = 0; s < n; s += 1024) {
-        int64_t i = s + threadIdx.x;
-        int64_t v = i < n ? in[i] : 0;
-        part[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            int64_t t = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-            __syncthreads();
-            part[threadIdx.x] += t;
-            __syncthreads();
-        }
-        if (i < n) out[i] = carry + part[threadIdx.x] - v;
-        __syncthreads();
-        if (threadIdx.x == 0) carry += part[1023];
-        __syncthreads();
+// Exclusive scan of int64 counts in three launches (no host sync, no inter-block
+// waiting): k_scan_reduce writes each 1024-element chunk's total into the first
+// output slot of the chunk, k_scan_chunks scans those totals in place (plus *base)
+// and writes the grand total, k_scan_apply scans each chunk and adds its offset.
+constexpr int kScanT = 1024;
+
+// inclusive scan over the block's 1024 threads (wave64 shuffles + 16 wave totals)
+__device__ __forceinline__ int64_t block_scan_incl(int64_t v, int64_t *wtot, int64_t *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
     }
+    if (lane == 63) wtot[wid] = v;
+    __syncthreads();
+    int64_t pre = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kScanT / 64; w++) {
+        const int64_t t = wtot[w];
+        pre += w < wid ? t : 0;
+        all += t;
+    }
+    __syncthreads();
+    *total = all;
+    return pre + v;
+}
+
+__global__ void __launch_bounds__(kScanT)
+k_scan_reduce(const int64_t *__restrict__ in, int64_t *__restrict__ out, int64_t n) {
+    __shared__ int64_t wtot[kScanT / 64];
+    const int64_t i = (int64_t)blockIdx.x * kScanT + threadIdx.x;
+    int64_t total;
+    (void)block_scan_incl(i < n ? in[i] : 0, wtot, &total);
+    if (threadIdx.x == 0) out[(int64_t)blockIdx.x * kScanT] = total;
+}
+
+__global__ void __launch_bounds__(kScanT)
+k_scan_chunks(int64_t *__restrict__ out, int64_t nchunks, const int64_t *base,
+              int64_t *total_out) {
+    __shared__ int64_t wtot[kScanT / 64];
+    int64_t carry = base ? base[0] : 0;      // read before total_out (may alias) is written
+    for (int64_t s = 0; s < nchunks; s += kScanT) {
+        const int64_t j = s + threadIdx.x;
+        const int64_t v = j < nchunks ? out[j * kScanT] : 0;
+        int64_t total;
+        const int64_t incl = block_scan_incl(v, wtot, &total);
+        if (j < nchunks) out[j * kScanT] = carry + incl - v;
+        carry += total;
+    }
+    __syncthreads();
     if (threadIdx.x == 0 && total_out) total_out[0] = carry;
+}
+
+// n <= 1024 in one launch (the side-effect rollouts' per-iteration pair of counts)
+__global__ void __launch_bounds__(kScanT)
+k_scan_small(const int64_t *__restrict__ in, int64_t *__restrict__ out, int64_t n,
+             const int64_t *base, int64_t *total_out) {
+    __shared__ int64_t wtot[kScanT / 64];
+    const int64_t carry = base ? base[0] : 0;
+    const int64_t i = threadIdx.x, v = i < n ? in[i] : 0;
+    int64_t total;
+    const int64_t incl = block_scan_incl(v, wtot, &total);
+    if (i < n) out[i] = carry + incl - v;
+    if (threadIdx.x == 0 && total_out) total_out[0] = carry + total;
+}
+
+__global__ void __launch_bounds__(kScanT)
+k_scan_apply(const int64_t *__restrict__ in, int64_t *__restrict__ out, int64_t n) {
+    __shared__ int64_t wtot[kScanT / 64];
+    __shared__ int64_t off;
+    const int64_t c0 = (int64_t)blockIdx.x * kScanT, i = c0 + threadIdx.x;
+    if (threadIdx.x == 0) off = out[c0];     // the chunk's offset (k_scan_chunks)
+    __syncthreads();
+    const int64_t v = i < n ? in[i] : 0;
+    int64_t total;
+    const int64_t incl = block_scan_incl(v, wtot, &total);
+    if (i < n) out[i] = off + incl - v;
 }
 
 // ---------------------------------------------------------------------------
@@ -375,8 +429,21 @@ extern "C" int sl_count_eligible(const uint16_t *in, int64_t *counts, int64_t B,
 extern "C" int sl_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n,
                                      const int64_t *base, int64_t *total_out, void *stream) {
     if (n < 0 || (n > 0 && (!in || !out))) return SL_EINVAL;
-    hipLaunchKernelGGL(k_scan_i64, dim3(1), dim3(1024), 0, (hipStream_t)stream, in, out, n,
-                       base, total_out);
+    hipStream_t s = (hipStream_t)stream;
+    if (n <= kScanT) {
+        hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kScanT), 0, s, in, out, n, base, total_out);
+        return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+    }
+    const int64_t nchunks = (n + kScanT - 1) / kScanT;
+    if (nchunks > 0x7FFFFFFF) return SL_EINVAL;
+    if (nchunks > 0) {
+        hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nchunks), dim3(kScanT), 0, s, in, out, n);
+        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+    }
+    hipLaunchKernelGGL(k_scan_chunks, dim3(1), dim3(kScanT), 0, s, out, nchunks, base, total_out);
+    if (hipGetLastError() != hipSuccess) return SL_EHIP;
+    if (nchunks > 0)
+        hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nchunks), dim3(kScanT), 0, s, in, out, n);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
@@ -460,7 +527,7 @@ extern "C" int sl_side_effect_densities(const uint16_t *init_board, const uint16
                 if (n_adv) {
                     hipLaunchKernelGGL(k_count_eligible, dim3((unsigned)n_adv), dim3(NT), lds, s,
                                        cur, ri, H, W);
-                    hipLaunchKernelGGL(k_scan_i64, dim3(1), dim3(1024), 0, s, ri, ri + 2,
+                    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kScanT), 0, s, ri, ri + 2,
                                        (int64_t)n_adv, stream_pos, stream_pos);
                 }
                 hipLaunchKernelGGL(k_rollout_advance<SL_RNG_STREAM>, dim3((unsigned)nb),

@@ -421,6 +421,7 @@ class SafeLifeVecEnv:
         longer match pool levels (kernels read them from HBM), the bit-plane
         mirrors are stale and the reset lists start empty."""
         self.st_t["start_roll"].fill_(-1)
+        self.st_t["spawn_flags"].fill_(3)    # may hold spawners: replay counts them
         self.planes_ok.zero_()
         self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()
         self._last_step = None

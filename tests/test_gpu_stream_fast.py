@@ -128,3 +128,23 @@ def test_fast_stream_exhaustion_flagged(torch_dev):
     for _ in range(3):
         venv.step(torch.zeros(8, dtype=torch.int32, device=dev))
     assert venv.stream_error()
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 1023, 1024, 1025, 4097, 131072, 262147])
+def test_exclusive_scan_i64(torch_dev, n):
+    """sl_exclusive_scan_i64 (the replay offsets): exclusive prefix sums plus a base,
+    the total written to a word that may alias the base (the stream position)."""
+    torch, dev = torch_dev
+    from safelife_amd import _lib
+    rng = np.random.RandomState(n)
+    counts = rng.randint(0, 3000, size=n).astype(np.int64)
+    src = torch.from_numpy(counts).to(dev)
+    out = torch.full((max(n, 1),), -7, dtype=torch.int64, device=dev)
+    pos = torch.tensor([123456789], dtype=torch.int64, device=dev)
+    _lib.check(_lib.lib().sl_exclusive_scan_i64(_lib.ptr(src), _lib.ptr(out), n, _lib.ptr(pos),
+                                                _lib.ptr(pos), _lib.stream_ptr(dev)),
+               "sl_exclusive_scan_i64")
+    torch.cuda.synchronize()
+    want = 123456789 + np.concatenate([[0], np.cumsum(counts)])
+    assert np.array_equal(out.cpu().numpy()[:n], want[:n])
+    assert int(pos.item()) == int(want[n])
