@@ -102,6 +102,7 @@ def lib():
                              u64, u32, u32, u32, vp, vp, vp]
     L.sl_count_eligible.argtypes = [vp, vp, i64, ctypes.c_int, ctypes.c_int, vp]
     L.sl_exclusive_scan_i64.argtypes = [vp, vp, i64, vp, vp, vp]
+    L.sl_copy16.argtypes = [vp, vp, i64, vp]
     L.sl_env_step.argtypes = [ctypes.POINTER(EnvState), ctypes.POINTER(LevelPool), vp,
                               ctypes.POINTER(EnvCfg), vp, vp, vp, vp, vp, vp]
     L.sl_env_reset.argtypes = [ctypes.POINTER(EnvState), ctypes.POINTER(LevelPool), vp,
@@ -124,7 +125,7 @@ def lib():
     for name in ("sl_event_create", "sl_event_destroy", "sl_event_elapsed_ms", "sl_device_arch", "sl_advance", "sl_count_eligible", "sl_exclusive_scan_i64",
                  "sl_env_step", "sl_env_reset", "sl_env_obs", "sl_level_pool_prepare",
                  "sl_side_effect_workspace", "sl_side_effect_densities",
-                 "sl_sample_actions", "sl_gae", "sl_emd_cells"):
+                 "sl_sample_actions", "sl_gae", "sl_emd_cells", "sl_copy16"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L
