@@ -148,3 +148,37 @@ def test_exclusive_scan_i64(torch_dev, n):
     want = 123456789 + np.concatenate([[0], np.cumsum(counts)])
     assert np.array_equal(out.cpu().numpy()[:n], want[:n])
     assert int(pos.item()) == int(want[n])
+
+
+@pytest.mark.parametrize("shape", [(3, 5), (7, 29), (9, 31), (20, 28), (17, 40)])
+def test_small_shapes_stream_vs_generic(torch_dev, shape):
+    """Replay on the small-board kernels at the shapes that exercise their corners: the
+    four-env waves with DPP neighbours (spare lanes holding wrap copies, odd W's
+    column-0 copy), the nl = 15 ds_bpermute form (W = 29), full 16-lane segments
+    (W = 31) and the one-env kernel (W = 40); batches that leave segments empty."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv
+    from test_gpu_parity import _synthetic_pool
+    H, W = shape
+    rng = np.random.RandomState(H * 97 + W)
+    pool = _synthetic_pool(rng, 6, H, W)
+    B, T = 37, 60
+    stream = np.random.RandomState(H + W).random_sample(3_000_000)
+    kw = dict(time_limit=21, view_shape=(9, 9), output_channels=None, penalty_coef=0.7,
+              min_performance=0.01, rng="stream", spawn_stream=stream, level_order="random",
+              augment_roll=True)
+    fast = SafeLifeVecEnv(pool, B, "cuda:0", kernel="fast", **kw)
+    gen = SafeLifeVecEnv(pool, B, "cuda:0", kernel="generic", **kw)
+    assert torch.equal(fast.reset(), gen.reset())
+    for t in range(T):
+        a = torch.from_numpy(rng.choice(9, size=B, p=[.05] + [.1] * 4 + [.1375] * 4)
+                             .astype(np.int32)).to(dev)
+        o1, r1, d1, _ = fast.step(a)
+        o2, r2, d2, _ = gen.step(a)
+        assert torch.equal(r1, r2), t
+        assert torch.equal(d1, d2), t
+        assert torch.equal(o1, o2), t
+        assert fast.stream_pos.item() == gen.stream_pos.item(), t
+        _compare_state(fast, gen, (shape, t))
+    assert fast.stream_pos.item() > 0
+    assert not fast.stream_error()
