@@ -84,9 +84,9 @@ int sl_event_create(void **ev);
 int sl_event_destroy(void *ev);
 int sl_event_elapsed_ms(void *begin, void *end, float *ms);   /* after completion */
 /* Bandwidth reference for roofline reporting (not on the env path): copies n16
- * 16-byte words src -> dst (dev, 16-B aligned) with a grid-stride vector kernel,
- * four loads in flight per lane -- what a plain streaming read+write of the same
- * bytes draws on this GPU. */
+ * 16-byte words src -> dst (dev, 16-B aligned) with a grid-stride vector kernel
+ * (1024 workgroups, one load per lane per iteration) -- what a plain streaming
+ * read+write of the same bytes draws on this GPU. */
 int sl_copy16(const void *src, void *dst, int64_t n16, void *stream);
 
 /* ---------------------------------------------------------------- boards -- */

@@ -91,12 +91,11 @@ __device__ __forceinline__ void load_pairs(const u32 *__restrict__ p, u32 D[32])
 #pragma unroll
     for (int y = 0; y < 32; y++) D[y] = p[y * S];
 }
-// the rows y with bit y of rm set (a wave-wide union) are written back
+// the same with the nontemporal cache policy (state read once per step)
 template <int S>
-__device__ __forceinline__ void store_pairs(u32 *__restrict__ p, const u32 D[32], u32 rm) {
+__device__ __forceinline__ void load_pairs_nt(const u32 *__restrict__ p, u32 D[32]) {
 #pragma unroll
-    for (int y = 0; y < 32; y++)
-        if ((rm >> y) & 1u) p[y * S] = D[y];
+    for (int y = 0; y < 32; y++) D[y] = __builtin_nontemporal_load(p + y * S);
 }
 
 template <int CTRL>

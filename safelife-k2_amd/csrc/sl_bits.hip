@@ -96,7 +96,7 @@ __device__ __forceinline__ void dma_board(const uint16_t *__restrict__ src, lds_
         const int c = (pos - ((row >> 5) << 2)) & 7;
         __builtin_amdgcn_global_load_lds((const void *)(s + row * 128 + c * 16),
                                          (__attribute__((address_space(3))) void *)(buf + k * 256),
-                                         16, 0, 0);
+                                         16, 0, 2);
     }
 }
 
@@ -495,7 +495,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
 #pragma unroll
             for (int q = 0; q < 32; q++) PG[q] = mg[q * 64];    // goal planes
         } else {
-            load_pairs<32>(gg, PG);                                 // goal cells
+            load_pairs_nt<32>(gg, PG);                              // goal cells
             transpose32(PG);
         }
         u32 cg[2];
@@ -519,7 +519,9 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         }
         if (rg) {
             transpose32(PG);
-            store_pairs<32>(gg, PG, rg);
+#pragma unroll
+            for (int y = 0; y < 32; y++)
+                if ((rg >> y) & 1u) __builtin_nontemporal_store(PG[y], &gg[y * 32]);
         }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -625,7 +627,11 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
             lds_put_board(buf, lane, PB);      // the start board in buf has been read out
         } else {
             transpose32(PB);
-            if (rb) store_pairs<32>(gb, PB, rb);
+            if (rb) {
+#pragma unroll
+                for (int y = 0; y < 32; y++)
+                    if ((rb >> y) & 1u) __builtin_nontemporal_store(PB[y], &gb[y * 32]);
+            }
             if (OBS) {      // bits 12-14 in use: add the goal colours bit-sliced
                 transpose32(PB);
 #pragma unroll

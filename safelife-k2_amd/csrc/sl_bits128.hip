@@ -247,7 +247,7 @@ k_env_step_bits128(Step128KArgs ka) {
 #pragma unroll 1
         for (int t = 0; t < NB; t++) {
             u32 G[32];
-            load_pairs<RS>(gg + 32 * t * RS, G);
+            load_pairs_nt<RS>(gg + 32 * t * RS, G);
             const u32 dn = t < NB - 1 ? gg[(32 * t + 32) * RS] : row0;
             if (t == 0) row0 = G[0];
             const u32 last = G[31];
@@ -272,7 +272,7 @@ k_env_step_bits128(Step128KArgs ka) {
 #pragma unroll
                 for (int y = 0; y < 32; y++)
                     if ((rg >> y) & 1u)
-                        if ((lm >> y) & 1u) gg[(32 * t + y) * RS] = G[y];
+                        if ((lm >> y) & 1u) __builtin_nontemporal_store(G[y], &gg[(32 * t + y) * RS]);
             }
         }
         const bool fixed = changed == 0 && __ballot(spawners != 0u) == 0ull;
@@ -305,7 +305,7 @@ k_env_step_bits128(Step128KArgs ka) {
 #pragma unroll 1
     for (int t = 0; t < NB; t++) {
         u32 P[32];
-        load_pairs<RS>(gb + 32 * t * RS, P);
+        load_pairs_nt<RS>(gb + 32 * t * RS, P);
         const u32 dn = t < NB - 1 ? gb[(32 * t + 32) * RS] : row0;
         if (roll >= 0) {
             wait_lgkm();        // the previous band's reads of the buffer are done
@@ -350,7 +350,7 @@ k_env_step_bits128(Step128KArgs ka) {
 #pragma unroll
             for (int y = 0; y < 32; y++)
                 if ((rb >> y) & 1u)
-                    if ((lm >> y) & 1u) gb[(32 * t + y) * RS] = P[y];
+                    if ((lm >> y) & 1u) __builtin_nontemporal_store(P[y], &gb[(32 * t + y) * RS]);
         }
     }
     const int points = wave_total(pts), score = wave_total(scr);

@@ -873,19 +873,13 @@ extern "C" int sl_event_elapsed_ms(void *begin, void *end, float *ms) {
 }
 
 namespace {
+// one 16-byte load per lane per iteration over 1024 workgroups: the fastest of the
+// copy shapes measured on MI355X (tools/bwtest.hip: 5.9 TB/s read + write; more
+// loads in flight or more workgroups 4.5-5.2)
 __global__ void __launch_bounds__(256) k_copy16(const uint4 *__restrict__ src,
                                                 uint4 *__restrict__ dst, int64_t n) {
     const int64_t stride = (int64_t)gridDim.x * 256;
-    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride],
-                    d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
-    }
-    for (; i < n; i += stride) dst[i] = src[i];
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) dst[i] = src[i];
 }
 }  // namespace
 
@@ -893,7 +887,7 @@ extern "C" int sl_copy16(const void *src, void *dst, int64_t n16, void *stream) 
     if (n16 < 0 || (n16 > 0 && (!src || !dst)) || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15))
         return SL_EINVAL;
     if (n16 == 0) return SL_OK;
-    hipLaunchKernelGGL(k_copy16, dim3(2048), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_copy16, dim3(1024), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)src, (uint4 *)dst, n16);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
