@@ -701,7 +701,7 @@ k_stream_prologue64(StepKArgs ka) {
     // creates one) draws nothing: its count is 0 without a read
     const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);     // toggling powers can make one
     u32 P[32];
-    if (spf & 1) load_pairs<32>(reinterpret_cast<const u32 *>(st.board + off) + lane_off, P);
+    if (spf & 1) load_pairs_nt<32>(reinterpret_cast<const u32 *>(st.board + off) + lane_off, P);
     OverlayT<GlobalCells> ov;
     ov.src.bd = st.board + off;
     ov.n = 0;
@@ -746,7 +746,7 @@ k_stream_prologue64(StepKArgs ka) {
 #pragma unroll
             for (int q = 0; q < 32; q++) P[q] = mg[q * 64];
         } else {
-            load_pairs<32>(reinterpret_cast<const u32 *>(st.goals + off) + lane_off, P);
+            load_pairs_nt<32>(reinterpret_cast<const u32 *>(st.goals + off) + lane_off, P);
             transpose32(P);
         }
         Geo64<SPAWN_COUNT> ggl{lane, StreamSrc{nullptr, 0, nullptr}, 0, 0};

@@ -418,7 +418,7 @@ k_stream_prologue128(Step128KArgs ka) {
             const int ru = (32 * t - 1) & (N - 1), rd = (32 * t + 32) & (N - 1);
             u32 up = g[ru * RS], dn = g[rd * RS];
             u32 P[32];
-            load_pairs<RS>(g + 32 * t * RS, P);
+            load_pairs_nt<RS>(g + 32 * t * RS, P);
             transpose32(P);
             if (edited && ne > 0) {
                 up = edit_row(up, ru, ne, eidx, eval, lane);

@@ -634,10 +634,13 @@ struct SegFields {
 // envs are consecutive, so each tensor's part is one contiguous block of 4 * H * W
 // u16 in HBM (it starts 8-byte aligned: b0 is a multiple of 4), copied dword by dword
 // with global_load_lds (no registers held, every copy in flight at once).  Tensor t
-// sits at u16 offset t * kSegStride of the stage, env e's cell (y, x) at e * H * W +
+// sits at u16 offset t * seg_stride(H, W) of the stage, env e's cell (y, x) at e * H * W +
 // y * W + x within it.
-constexpr int kSegStride = 4 * 32 * 32 + 128;       // u16 per staged tensor (4 envs,
-                                                     // 64-dword DMA granules)
+// u16 per staged tensor: the four envs' 4 * H * W cells rounded up to whole 64-dword
+// DMA granules (the clamped lanes of the last granule write up to its end)
+__host__ __device__ __forceinline__ int seg_stride(int H, int W) {
+    return 128 * ((2 * H * W + 63) / 64);
+}
 __device__ __forceinline__ void dma_seg(const sl_env_state &st, int64_t b0, int nenv,
                                         lds_u32 *stage, int lane) {
     const int64_t HW = (int64_t)st.H * st.W;
@@ -646,7 +649,7 @@ __device__ __forceinline__ void dma_seg(const sl_env_state &st, int64_t b0, int 
 #pragma unroll
     for (int t = 0; t < 3; t++) {
         const char *g = reinterpret_cast<const char *>(src[t]);
-        lds_u32 *dst = stage + t * (kSegStride / 2);
+        lds_u32 *dst = stage + t * (seg_stride(st.H, st.W) / 2);
         for (int k = 0; k * 64 < nd; k++) {
             const int d = k * 64 + lane;
             __builtin_amdgcn_global_load_lds((const void *)(g + 4 * (d < nd ? d : 0)),
@@ -664,7 +667,8 @@ __device__ __forceinline__ void dma_seg_tail(const sl_env_state &st, int64_t b0,
     if ((n & 1) && lane < 3) {
         const uint16_t *src = (lane == 0 ? st.board : lane == 1 ? st.goals : st.start_board) +
                               b0 * HW;
-        reinterpret_cast<lds_u16 *>(stage + lane * (kSegStride / 2))[n - 1] = src[n - 1];
+        reinterpret_cast<lds_u16 *>(stage + lane * (seg_stride(st.H, st.W) / 2))[n - 1] =
+            src[n - 1];
     }
 }
 
@@ -699,7 +703,8 @@ k_env_step_seg4(SmallKArgs ka) {
     extern __shared__ __attribute__((aligned(16))) u32 dyn_stage[];
     lds_u16 *stage = (lds_u16 *)dyn_stage;
     const int env_off = e * H * W;
-    lds_u16 *sb = stage + env_off, *sg = sb + kSegStride, *ss = sg + kSegStride;
+    const int sstride = seg_stride(H, W);
+    lds_u16 *sb = stage + env_off, *sg = sb + sstride, *ss = sg + sstride;
 
     // the column pair this lane holds: its own, or (DPPN) the copy a rotation needs
     const int js = j < nl ? j : (DPPN ? (j == 15 ? nl - 1 : (j == nl ? 0 : -1)) : -1);
@@ -982,7 +987,7 @@ int launch_step_small(const sl_env_state &st, const StepArgs &a, const FastExtra
     const bool seg = st.W <= kSegW;
     const bool dppn = (st.W + 1) / 2 != 15;      // GeoSeg: DPP neighbours unless nl = 15
     const dim3 grid4((unsigned)((st.B + 3) / 4));
-    const size_t lds4 = (size_t)3 * kSegStride * sizeof(uint16_t);
+    const size_t lds4 = (size_t)3 * seg_stride(st.H, st.W) * sizeof(uint16_t);
     if (fx.stream) {
         hipLaunchKernelGGL(k_stream_prologue_small, grid, dim3(64), lds, s, ka);
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
