@@ -13,8 +13,10 @@
 //  * the rows just outside a band (32t-1 and 32t+32, wrapping at H = 128) enter the
 //    rule as halo words (bit 31 = the row above, bit 0 = the row below): every 3x3
 //    quantity the rule folds is evaluated on the band's planes and on the halo
-//    planes, and a funnel shift (v_alignbit) joins them.  The eight halo rows are
-//    read before any band is written back, so every band sees the pre-step board;
+//    planes, and a funnel shift (v_alignbit) joins them.  Bands run in order, so a
+//    band's upper halo is the previous band's last row (kept from its load) and its
+//    lower halo the next band's first row (not yet written); every band sees the
+//    pre-step board;
 //  * points, performance score, possible score and side effects
 //    (safelife_game.py:590-631, env_wrappers.py:319-342) are summed band by band;
 //    only the 64-byte row sectors that changed are stored (16 lanes' words);
@@ -22,9 +24,10 @@
 //    holds their planes.  Goals without spawners that came through a step unchanged
 //    are at a fixed point of the rule (planes_ok bit 2): the rule is skipped and only
 //    their three colour planes are read, per band, for the scores;
-//  * the action (execute_action / move_agent, safelife_game.py:308-393) runs on lane
-//    0 against the board in HBM before any band is stored; its cell edits are
-//    broadcast and written into the band planes and halo rows before the rule;
+//  * the action (execute_action / move_agent, safelife_game.py:308-393) has run
+//    before this kernel: k_env_action (one lane per env) or, in replay mode,
+//    k_stream_prologue128 leaves the state and cell edits in HBM and the reward in
+//    the scratch;
 //  * exits are rewritten by the epilogue after the band stores have completed.
 // Finished envs are queued and reset by a follow-up kernel (k_env_reset_list_wide,
 // one 1024-thread block per env).
