@@ -196,6 +196,90 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
 }
 
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+// LDS slots compact_draws needs: one per 2x2 block a wave can hold (64 lanes x 16)
+constexpr int kDrawSlots = 1024;
+
+// The same draws as lane_draws, with the wave's eligible blocks spread over all its
+// lanes.  Spawning cells cluster round the spawners, so a few lanes hold most blocks
+// and lane_draws runs as many Philox evaluations as the busiest lane has blocks
+// (C5 steady state: 28 per env-step) while the other lanes idle; here the wave runs
+// ceil(blocks / 64) (C5: 10).  Each lane queues its blocks as (lane, y / 2) in the
+// LDS slots from its exclusive prefix (the counts' bits by ballot + v_mbcnt), lane i
+// of round r evaluates slot 64 r + i (the block number from Geo::block_of) and writes
+// its four compare bits into the slot's top nibble, and the owner reads them back.
+// The wave is the whole workgroup; LDS operations of one wave execute in order.
+template <class Geo>
+__device__ __forceinline__ void compact_draws(const Geo &g, const u32 elig[2], u32 sp[2],
+                                              const SpawnCtx &sc, u32 tensor, lds_u16 *slots) {
+    const u32 lim = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(ceil(sc.thr * 4294967296.0) - 1.0));
+    const u32 any = elig[0] | elig[1];
+    const u32 blocks = (any | (any >> 1)) & 0x55555555u;
+    const int cnt = __builtin_popcount(blocks);
+    int pre = 0, total = 0;
+#pragma unroll
+    for (int bit = 0; bit < 5; bit++) {         // cnt <= 16
+        const uint64_t m = __ballot((cnt >> bit) & 1);
+        pre += lanes_below(m) << bit;
+        total += __builtin_popcountll(m) << bit;
+    }
+    const int lane = (int)__lane_id();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // the last call's reads
+    __builtin_amdgcn_wave_barrier();
+    {
+        u32 m = blocks;
+        int k = pre;
+        while (m) {
+            const int y = __builtin_ctz(m);
+            m &= m - 1;
+            slots[k++] = (uint16_t)((lane << 4) | (y >> 1));
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+    for (int base = 0; base < total; base += 64) {
+        const int i = base + lane;
+        if (i < total) {
+            const u32 it = slots[i];
+            uint32_t r[4];
+            philox4x32(g.block_of((int)(it >> 4), (int)(it & 15u) << 1), sc.gid, sc.step, tensor,
+                       sc.seed, r);
+            const u32 res = (r[0] <= lim ? 1u : 0u) | (r[1] <= lim ? 2u : 0u) |
+                            (r[2] <= lim ? 4u : 0u) | (r[3] <= lim ? 8u : 0u);
+            slots[i] = (uint16_t)(it | (res << 12));
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    u32 s0 = 0u, s1 = 0u;
+    {
+        u32 m = blocks;
+        int k = pre;
+        while (m) {
+            const int y = __builtin_ctz(m);
+            m &= m - 1;
+            const u32 res = (u32)slots[k++] >> 12;
+            s0 |= ((res & 1u) | ((res >> 1) & 2u)) << y;      // r[0]: row y, r[2]: row y + 1
+            s1 |= (((res >> 1) & 1u) | ((res >> 2) & 2u)) << y;
+        }
+    }
+    sp[0] = s0 & elig[0];
+    sp[1] = s1 & elig[1];
+}
+template <class Geo>
+__device__ __forceinline__ void philox_spawn_compact(const Geo &g, const u32 elig[2], u32 sp[2],
+                                                     const SpawnCtx &sc, u32 tensor,
+                                                     lds_u16 *slots) {
+    if (sc.thr <= 0.0) {
+    } else if (sc.thr >= 1.0) {
+        sp[0] = elig[0];
+        sp[1] = elig[1];
+    } else {
+        compact_draws(g, elig, sp, sc, tensor, slots);
+    }
+}
+
 // Reference-order draws (SL_RNG_STREAM; random.c:47-52 consumed by advance_board.c:
 // 109-113): the eligible cells of a tensor take the uniforms draws[pos], draws[pos+1],
 // ... in row-major order -- one per eligible cell whatever p is -- and spawn iff

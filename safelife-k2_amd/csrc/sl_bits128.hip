@@ -72,6 +72,7 @@ struct GeoBand {
     int64_t pos;       // used = how many the band consumed
     int used;
     int count;         // SPAWN_COUNT: this lane's eligible cells
+    lds_u16 *slots;    // SPAWN_PHILOX: compact_draws' queue (kDrawSlots)
     template <class F>
     __device__ __forceinline__ V3 vert(const u32 *P, int w, F f) const {
         return vert_with(f(P, w), f(hv, w));
@@ -84,12 +85,15 @@ struct GeoBand {
     }
     // the 2x2 spawn block of band rows y, y + 1 (y even) of the lane's column pair
     __device__ __forceinline__ u32 block(int y) const {
-        return (u32)(((row0 + y) >> 1) * (N / 2) + lane);
+        return block_of(lane, y);
+    }
+    __device__ __forceinline__ u32 block_of(int l, int y) const {
+        return (u32)(((row0 + y) >> 1) * (N / 2) + l);
     }
     __device__ __forceinline__ void spawn(const u32 elig[2], u32 sp[2], const SpawnCtx &sc,
                                           u32 tensor) {
         if (MODE == SPAWN_PHILOX) {
-            philox_spawn(*this, elig, sp, sc, tensor);
+            philox_spawn_compact(*this, elig, sp, sc, tensor, slots);
         } else if (MODE == SPAWN_STREAM) {
             used = stream_draws<false>(elig, sp, sc.thr, src, pos, lane);
         } else {
@@ -221,6 +225,8 @@ k_env_step_bits128(Step128KArgs ka) {
     const u32 V = load_record(st, ka.actions, b, lane);
     __shared__ __attribute__((aligned(16))) u32 spool_[kPoolPlanes * 256];
     __attribute__((address_space(3))) u32 *spool = (__attribute__((address_space(3))) u32 *)spool_;
+    __shared__ uint16_t slots_[kDrawSlots];
+    lds_u16 *slots = (lds_u16 *)slots_;
     const int pok = rec(V, R_POK) & 6;
     const Scratch w = scratch_of(fx.scratch, st.B);
 
@@ -256,7 +262,7 @@ k_env_step_bits128(Step128KArgs ka) {
             const u32 last = G[31];
             transpose32(G);
             u32 cg[2];
-            GeoBand<MODE> geo{lane, 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_g, 0, 0};
+            GeoBand<MODE> geo{lane, 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_g, 0, 0, slots};
             rule_planes(G, cg, geo, sc, 1u);
             pos_g += geo.used;
             up = last;
@@ -318,7 +324,7 @@ k_env_step_bits128(Step128KArgs ka) {
         const u32 last = P[31];
         transpose32(P);
         u32 cb[2];
-        GeoBand<MODE> geo{lane, 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_b, 0, 0};
+        GeoBand<MODE> geo{lane, 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_b, 0, 0, slots};
         rule_planes(P, cb, geo, sc, 0u);
         pos_b += geo.used;
         up = last;
@@ -428,7 +434,7 @@ k_stream_prologue128(Step128KArgs ka) {
                 dn = edit_row(dn, rd, ne, eidx, eval, lane);
                 (void)apply_edits(P, ne, eidx, eval, 32 * t, lane);
             }
-            GeoBand<SPAWN_COUNT> geo{lane, 32 * t, HaloView{up, dn}, none, 0, 0, 0};
+            GeoBand<SPAWN_COUNT> geo{lane, 32 * t, HaloView{up, dn}, none, 0, 0, 0, nullptr};
             u32 ch[2];
             rule_planes(P, ch, geo, sc, 0u);
             n += geo.count;

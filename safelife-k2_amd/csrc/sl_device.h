@@ -27,9 +27,9 @@ constexpr uint32_t POWERS = ALIVE | INHIBIT | PRESERVE | SPAWN;
 __device__ __forceinline__ void philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                            uint64_t seed, uint32_t out[4]) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    // rolled: unrolled inside the bit-sliced kernels' draw loops it costs the 64x64
-    // kernel 64 spilled VGPRs
-#pragma unroll 1
+    // two rounds per iteration (no register rotation moves); fully unrolled inside the
+    // bit-sliced kernels' draw loops it cost the 64x64 kernel 64 spilled VGPRs
+#pragma unroll 2
     for (int r = 0; r < 10; r++) {
         uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
         uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
