@@ -197,16 +197,10 @@ __device__ __forceinline__ u32 mux_edits(u32 P[32], int ne, const int eidx[4], c
 // over it; the exit list is collected row by row in np.nonzero order.
 __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_level_pool &pool,
                                         const ResetArgs &ra, int64_t b, int lane) {
-    int li = 0, dy = 0, dx = 0;
-    if (lane == 0) {
-        const LevelChoice c = choose_level(pool, ra, ra.env0 + (uint32_t)b, st.episodes[b], N, N);
-        li = c.idx;
-        dy = c.dy;
-        dx = c.dx;
-    }
-    li = __builtin_amdgcn_readfirstlane(li);
-    dy = __builtin_amdgcn_readfirstlane(dy);
-    dx = __builtin_amdgcn_readfirstlane(dx);
+    const int ep = __builtin_amdgcn_readfirstlane(st.episodes[b]);
+    const LevelChoice lc = choose_level_wave(pool, ra, ra.env0 + (uint32_t)b, ep, N, N, lane);
+    const int li = lc.idx, dy = lc.dy, dx = lc.dx;
+    const LevelScalars ls = level_scalars(pool, li);     // in flight with the gathers
     const int h = lane & 1, j = lane >> 1;
     const uint16_t *lb = pool.board + (int64_t)li * (N * N), *lg = pool.goals + (int64_t)li * (N * N);
     const int c0 = (2 * j - dx) & 63, c1 = (2 * j + 1 - dx) & 63;
@@ -259,8 +253,8 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
     const bool sb = __ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull;
     int ev = 0;
     if (lane == 0)
-        ev = reset_scalars(st, pool, ra, b, li, dy, dx, (s1 & 0xFFFF) - 192 * 64,
-                           ((s1 >> 16) & 0xFFFF) - 64 * 64, s2, (sb ? 1 : 0) | (sg ? 2 : 0));
+        ev = reset_scalars_from(st, ra, b, li, dy, dx, ls, ep, (s1 & 0xFFFF) - 192 * 64,
+                                ((s1 >> 16) & 0xFFFF) - 64 * 64, s2, (sb ? 1 : 0) | (sg ? 2 : 0));
     ev = __builtin_amdgcn_readfirstlane(ev);
     const u32 ex0 = PL(P, 8, 0), ex1 = PL(P, 8, 1);       // exit planes
     // the board: the start board with its exits coloured (update_exit_colors)
@@ -768,10 +762,13 @@ k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scr
                  uint32_t step, sl::obs::ObsArgs oa, uint16_t *obs_out) {
     int64_t *cnt = scratch + 8 * st.B + 2;
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(step + 1) & 1] = 0;
-    const int n = (int)__builtin_amdgcn_readfirstlane((int)cnt[step & 1]);
     const int32_t *list = reset_list(scratch);
+    // the first entry is loaded together with the length (grid <= B <= list size; the
+    // value is used only when the entry is in the list)
+    const int first = list[blockIdx.x];
+    const int n = (int)__builtin_amdgcn_readfirstlane((int)cnt[step & 1]);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
-        const int64_t b = __builtin_amdgcn_readfirstlane(list[i]);
+        const int64_t b = __builtin_amdgcn_readfirstlane(i == (int)blockIdx.x ? first : list[i]);
         wave_reset(st, pool, ra, b, threadIdx.x);
         if (obs_out) {
             wait_vm();      // the reset's stores have landed (no stale lines: this wave

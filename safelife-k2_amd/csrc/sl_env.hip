@@ -403,12 +403,18 @@ __device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, co
                            int64_t b, WideResetShared &sh) {
     const int H = st.H, W = st.W, hw = H * W;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (tid == 0) {
-        const LevelChoice c = choose_level(pool, a, a.env0 + (uint32_t)b, st.episodes[b], H, W);
-        sh.idx = c.idx;
-        sh.dy = c.dy;
-        sh.dx = c.dx;
-        sh.nex = 0;
+    int ep = 0;
+    LevelScalars ls{};
+    if (wid == 0) {        // the three Philox draws side by side on lanes 0-2
+        ep = __builtin_amdgcn_readfirstlane(st.episodes[b]);
+        const LevelChoice c = choose_level_wave(pool, a, a.env0 + (uint32_t)b, ep, H, W, lane);
+        ls = level_scalars(pool, c.idx);      // thread 0's, in flight with the gathers
+        if (lane == 0) {
+            sh.idx = c.idx;
+            sh.dy = c.dy;
+            sh.dx = c.dx;
+            sh.nex = 0;
+        }
     }
     __syncthreads();
     const int idx = sh.idx, dy = sh.dy, dx = sh.dx;
@@ -441,7 +447,7 @@ __device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, co
         for (int w = 0; w < NTR / 64; w++)
             for (int k = 0; k < 4; k++) t[k] += sh.red[w][k];
         const int spawn_bits = ((t[3] & 0xFFFF) ? 1 : 0) | ((t[3] >> 16) ? 2 : 0);
-        sh.ev = reset_scalars(st, pool, a, b, idx, dy, dx, t[0], t[1], t[2], spawn_bits);
+        sh.ev = reset_scalars_from(st, a, b, idx, dy, dx, ls, ep, t[0], t[1], t[2], spawn_bits);
         const int nex = sh.nex;
         int16_t *ey = st.exit_y + b * SL_MAX_EXITS, *ex = st.exit_x + b * SL_MAX_EXITS;
         int n = 0;

@@ -196,6 +196,46 @@ __device__ __forceinline__ LevelChoice choose_level(const sl_level_pool &pool, c
     return LevelChoice{idx, dy, dx};
 }
 
+// choose_level by a whole wave: lane 0 picks the level, lanes 1 and 2 the roll, so
+// the three Philox draws run side by side instead of one after another on one lane.
+// Every lane returns the same choice, bit-identical to choose_level's.
+__device__ __forceinline__ LevelChoice choose_level_wave(const sl_level_pool &pool,
+                                                        const ResetArgs &a, uint32_t gid,
+                                                        int ep, int H, int W, int lane) {
+    const uint32_t key = lane == 0 ? 0x5EEDu : (lane == 1 ? 0x0011u : 0x0022u);
+    const double u = philox_uniform(gid, (uint32_t)ep, key, lane == 0 ? 2u : 3u, a.seed);
+    int v;
+    if (lane == 0) {
+        v = a.level_mode == 1 ? (int)(u * pool.K)
+                              : (int)(((int64_t)gid + (int64_t)ep * a.n_total) % pool.K);
+        v = min(max(v, 0), pool.K - 1);
+    } else {
+        const int n = lane == 1 ? H : W;
+        v = a.augment ? min((int)(u * n), n - 1) : 0;
+    }
+    return LevelChoice{__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 1),
+                       __builtin_amdgcn_readlane(v, 2)};
+}
+
+// the pool fields of level idx a reset copies into the env's scalars; loaded as soon
+// as the level is known, so they arrive while the board gathers are in flight
+struct LevelScalars {
+    double mp;
+    int ax, ay, orientation;
+    float spawn_prob;
+};
+
+__device__ __forceinline__ LevelScalars level_scalars(const sl_level_pool &pool, int idx) {
+    return LevelScalars{pool.min_performance[idx], pool.agent_x[idx], pool.agent_y[idx],
+                        pool.orientation[idx], pool.spawn_prob[idx]};
+}
+
+__device__ __forceinline__ uint16_t reset_scalars_from(const sl_env_state &st, const ResetArgs &a,
+                                                       int64_t b, int idx, int dy, int dx,
+                                                       const LevelScalars &ls, int ep,
+                                                       int points, int base, int possible,
+                                                       int spawn_bits);
+
 // Per-env scalar state of a fresh episode (SafeLifeEnv.reset + revert,
 // safelife_env.py:188-198, safelife_game.py:196-212; MovementBonusWrapper.reset and
 // SimpleSideEffectPenalty.reset, env_wrappers.py:90-94,313-317).  One thread.
@@ -206,13 +246,24 @@ __device__ __forceinline__ uint16_t reset_scalars(const sl_env_state &st,
                                                   const sl_level_pool &pool, const ResetArgs &a,
                                                   int64_t b, int idx, int dy, int dx, int points,
                                                   int base, int possible, int spawn_bits) {
+    return reset_scalars_from(st, a, b, idx, dy, dx, level_scalars(pool, idx), st.episodes[b],
+                              points, base, possible, spawn_bits);
+}
+
+// the same from the level's fields already loaded (level_scalars) and the env's
+// episode count `ep` as read before the reset
+__device__ __forceinline__ uint16_t reset_scalars_from(const sl_env_state &st, const ResetArgs &a,
+                                                       int64_t b, int idx, int dy, int dx,
+                                                       const LevelScalars &ls, int ep,
+                                                       int points, int base, int possible,
+                                                       int spawn_bits) {
     const int H = st.H, W = st.W;
-    const double lvl_mp = pool.min_performance[idx];
+    const double lvl_mp = ls.mp;
     const bool can = can_exit_now(lvl_mp, base, base, possible);
-    const int ax = pymod(pool.agent_x[idx] + dx, W), ay = pymod(pool.agent_y[idx] + dy, H);
+    const int ax = pymod(ls.ax + dx, W), ay = pymod(ls.ay + dy, H);
     st.agent_x[b] = ax;
     st.agent_y[b] = ay;
-    st.orientation[b] = pool.orientation[idx];
+    st.orientation[b] = ls.orientation;
     st.game_over[b] = 0;
     st.num_steps[b] = 0;
     st.spawn_flags[b] = ((spawn_bits & 1) || a.toggle_powers ? 1 : 0) | (spawn_bits & 2);
@@ -223,7 +274,7 @@ __device__ __forceinline__ uint16_t reset_scalars(const sl_env_state &st,
     st.score[b] = base;
     st.possible[b] = possible;
     st.side_effect[b] = 0;
-    st.spawn_prob[b] = pool.spawn_prob[idx];
+    st.spawn_prob[b] = ls.spawn_prob;
     st.min_performance[b] = isnan(a.wrapper_min_perf) ? lvl_mp : a.wrapper_min_perf;
     st.prior_x[b * SL_BONUS_PERIOD_MAX] = ax;
     st.prior_y[b * SL_BONUS_PERIOD_MAX] = ay;
@@ -232,7 +283,7 @@ __device__ __forceinline__ uint16_t reset_scalars(const sl_env_state &st,
     st.level_index[b] = idx;
     if (st.start_roll) st.start_roll[b] = (dy << 16) | dx;
     if (st.planes_ok) st.planes_ok[b] = 0;    // the 64x64 reset re-validates
-    st.episodes[b] = st.episodes[b] + 1;
+    st.episodes[b] = ep + 1;
     return (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
 }
 
