@@ -437,7 +437,7 @@ __device__ __forceinline__ void issue_pre(const sl_env_state &st, const int32_t 
 
 // One env-step of env b.  `pre` holds b's record and goal colour planes and b's board
 // is in flight into `buf` (issued by the caller).  MODE: SPAWN_PHILOX, or SPAWN_STREAM
-// (replay: k_stream_prologue64 has run the action and sized the draws; the step reads
+// (replay: k_env_action has run the action and k_stream_prologue64 sized the draws; the step reads
 // act[b] and each tensor's first uniform from the scratch words).
 template <bool OBS, int MODE>
 __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs &a,
@@ -538,7 +538,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
                rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     int act_reward = 0;
-    if (MODE == SPAWN_STREAM) {        // the prologue ran the action (no edits left)
+    if (MODE == SPAWN_STREAM) {        // k_env_action ran the action (no edits left)
         act_reward = (int)scratch_of(fx.scratch, st.B).act[b];
     } else {
         if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ctp, ctc, ov);
@@ -678,11 +678,14 @@ k_env_step_bits64(StepKArgs ka) {
                   ka.done_out, ka.flags_out, ka.ep_len_out, ka.ep_rew_out, pre);
 }
 
-// Replay-mode prologue of env b (SL_RNG_STREAM), one wave: the action (state, its
-// cell edits into the board in HBM, its reward into scratch act[b]), then the eligible
-// cells -- the uniforms the step will draw -- of the acted-on board and of the goals
-// (scratch counts[2b], [2b+1]; sl_exclusive_scan_i64 turns them into each tensor's first
-// uniform).  The work of k_env_action + k_env_count (sl_env.hip) on the bit-sliced rule.
+// Replay-mode count of env b (SL_RNG_STREAM), one wave, after k_env_action (one lane
+// per env) has applied the actions -- state and cell edits in HBM, rewards in scratch
+// act[] -- so the board read here is the acted-on one: the eligible cells, i.e. the
+// uniforms the step will draw, of the board and of the goals (scratch counts[2b],
+// [2b+1]; sl_exclusive_scan_i64 turns them into each tensor's first uniform).  The work
+// of k_env_count (sl_env.hip) on the bit-sliced rule.  (The action ran on lane 0 of
+// this wave before: one wave per env for a one-lane latency chain made this launch
+// cost as much as a quarter of the step on boards without spawners.)
 __global__ void __launch_bounds__(64)
 k_stream_prologue64(StepKArgs ka) {
     const sl_env_state &st = ka.st;
@@ -691,42 +694,16 @@ k_stream_prologue64(StepKArgs ka) {
     const int64_t off = b * (int64_t)(N * N);
     const int lane_off = (lane & 1) * 1024 + (lane >> 1);
     const u32 V = load_record(st, ka.actions, b, lane);
+    const Scratch w = scratch_of(ka.fx.scratch, st.B);
     // a board or goals without spawners (spawn_flags, set at reset: no rule or action
     // creates one) draws nothing: its count is 0 without a read
     const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);     // toggling powers can make one
-    u32 P[32];
-    if (spf & 1) load_pairs_nt<32>(reinterpret_cast<const u32 *>(st.board + off) + lane_off, P);
-    OverlayT<GlobalCells> ov;
-    ov.src.bd = st.board + off;
-    ov.n = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        ov.idx[k] = 0;
-        ov.val[k] = 0;
-    }
-    RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
-               rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
-    const Scratch w = scratch_of(ka.fx.scratch, st.B);
-    if (lane == 0) {
-        w.act[b] = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
-        // the edits: into HBM for the step kernel, into the planes below for the count
-        // (whether the wave's loads saw these stores does not matter)
-        for (int k = 0; k < ov.n; k++) st.board[off + ov.idx[k]] = (uint16_t)ov.val[k];
-    }
-    const int ne = __builtin_amdgcn_readfirstlane(ov.n);
-    int eidx[4];
-    u32 eval[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        eidx[k] = __builtin_amdgcn_readfirstlane(ov.idx[k]);
-        eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
-    }
     SpawnCtx sc{0u, 0u, 0ull, 0.0};
-    u32 ch[2];
+    u32 P[32], ch[2];
     int nb = 0;
     if (spf & 1) {
+        load_pairs_nt<32>(reinterpret_cast<const u32 *>(st.board + off) + lane_off, P);
         transpose32(P);
-        (void)mux_edits(P, ne, eidx, eval, lane);
         Geo64<SPAWN_COUNT> gbd{lane, StreamSrc{nullptr, 0, nullptr}, 0, 0};
         rule_planes(P, ch, gbd, sc, 0u);
         nb = wave_total(gbd.count);
@@ -791,6 +768,8 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
     if (fx.obs_out && (fx.obs_vh < 1 || fx.obs_vw < 1 || fx.obs_vh * fx.obs_vw > 4096))
         return SL_EINVAL;
     if (fx.stream) {
+        const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
+        if (rca) return rca;
         hipLaunchKernelGGL(k_stream_prologue64, dim3(grid), dim3(64), 0, s, ka);
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
         const int rc = stream_offsets(st, fx, s);

@@ -25,9 +25,9 @@
 //    are at a fixed point of the rule (planes_ok bit 2): the rule is skipped and only
 //    their three colour planes are read, per band, for the scores;
 //  * the action (execute_action / move_agent, safelife_game.py:308-393) has run
-//    before this kernel: k_env_action (one lane per env) or, in replay mode,
-//    k_stream_prologue128 leaves the state and cell edits in HBM and the reward in
-//    the scratch;
+//    before this kernel: k_env_action (one lane per env, both RNG modes) leaves the
+//    state and cell edits in HBM and the reward in the scratch (in replay mode
+//    k_stream_prologue128 then counts the draws);
 //  * exits are rewritten by the epilogue after the band stores have completed.
 // Finished envs are queued and reset by a follow-up kernel (k_env_reset_list_wide,
 // one 1024-thread block per env).
@@ -102,47 +102,6 @@ struct GeoBand {
     }
 };
 
-// Applies the action's cell edits (wave-uniform (flat index, value) pairs) to band
-// t's planes on the lane owning the cell; returns the band rows (bit y) edited.
-__device__ __forceinline__ u32 apply_edits(u32 P[32], int ne, const int eidx[4],
-                                           const u32 eval[4], int row0, int lane) {
-    u32 erow = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        if (k < ne) {
-            const int y = (eidx[k] >> 7) - row0, x = eidx[k] & (N - 1);
-            if (y >= 0 && y < 32) {
-                const u32 bit = 1u << y;
-                const bool mine = lane == (x >> 1);
-                const u32 m0 = (mine && !(x & 1)) ? bit : 0u;
-                const u32 m1 = (mine && (x & 1)) ? bit : 0u;
-                erow |= bit;
-#pragma unroll
-                for (int p = 0; p < 16; p++) {
-                    const u32 v = ((eval[k] >> p) & 1u) ? ~0u : 0u;
-                    PL(P, p, 0) = mux(m0, v, PL(P, p, 0));
-                    PL(P, p, 1) = mux(m1, v, PL(P, p, 1));
-                }
-            }
-        }
-    }
-    return erow;
-}
-
-// the same edits on a halo row's raw cell pair (row index r)
-__device__ __forceinline__ u32 edit_row(u32 d, int r, int ne, const int eidx[4],
-                                        const u32 eval[4], int lane) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        if (k < ne && (eidx[k] >> 7) == r) {
-            const int x = eidx[k] & (N - 1);
-            if (lane == (x >> 1))
-                d = (x & 1) ? (d & 0x0000FFFFu) | (eval[k] << 16) : (d & 0xFFFF0000u) | eval[k];
-        }
-    }
-    return d;
-}
-
 // The start-board planes the side-effect term reads (0, 2, 7-15), from the level
 // pool's bit planes when the env was reset from the pool: row y of
 // band t is level row 32t + y - dy, one funnel shift of two adjacent 32-row words;
@@ -203,8 +162,7 @@ __device__ __forceinline__ const Step128KArgs &kargs128() {
     return *(const Step128KArgs *)kp;
 }
 
-// One env-step of env b, after the action: k_env_action (Philox mode) or
-// k_stream_prologue128 (replay) has applied it -- state and cell edits in HBM, reward
+// One env-step of env b, after the action: k_env_action has applied it -- state and cell edits in HBM, reward
 // in scratch act[b] -- so this kernel holds no action code, no edit lists and no
 // overlay.  MODE: SPAWN_PHILOX, or SPAWN_STREAM (each tensor's first uniform from the
 // scratch offsets).
@@ -377,11 +335,12 @@ k_env_step_bits128(Step128KArgs ka) {
     }
 }
 
-// Replay-mode prologue of env b (SL_RNG_STREAM), one wave: the action (state, its
-// cell edits into the board in HBM, its reward into scratch act[b]), then the eligible
-// cells of the acted-on board and of the goals, band by band (scratch counts[2b],
-// [2b+1]; sl_exclusive_scan_i64 turns them into each tensor's first uniform).  The work of
-// k_env_action + k_env_count (sl_env.hip) on the bit-sliced rule.
+// Replay-mode count of env b (SL_RNG_STREAM), one wave, after k_env_action (one lane
+// per env) has applied the actions -- state and cell edits in HBM, rewards in scratch
+// act[] -- so the board read here is the acted-on one: the eligible cells of the board
+// and of the goals, band by band (scratch counts[2b], [2b+1]; sl_exclusive_scan_i64
+// turns them into each tensor's first uniform).  The work of k_env_count (sl_env.hip)
+// on the bit-sliced rule.
 __global__ void __launch_bounds__(64)
 k_stream_prologue128(Step128KArgs ka) {
     const sl_env_state &st = ka.st;
@@ -391,48 +350,19 @@ k_stream_prologue128(Step128KArgs ka) {
     const u32 *gb = reinterpret_cast<const u32 *>(st.board + off) + lane;
     const u32 *gg = reinterpret_cast<const u32 *>(st.goals + off) + lane;
     const u32 V = load_record(st, ka.actions, b, lane);
-    OverlayT<GlobalCells> ov;
-    ov.src.bd = st.board + off;
-    ov.n = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        ov.idx[k] = 0;
-        ov.val[k] = 0;
-    }
-    RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
-               rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     const Scratch w = scratch_of(ka.fx.scratch, st.B);
-    if (lane == 0) {
-        w.act[b] = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
-        // into HBM for the step kernel; into the planes and halo rows below for the
-        // count (whether this wave's loads see these stores does not matter)
-        for (int k = 0; k < ov.n; k++) st.board[off + ov.idx[k]] = (uint16_t)ov.val[k];
-    }
-    const int ne = __builtin_amdgcn_readfirstlane(ov.n);
-    int eidx[4];
-    u32 eval[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        eidx[k] = __builtin_amdgcn_readfirstlane(ov.idx[k]);
-        eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
-    }
     SpawnCtx sc{0u, 0u, 0ull, 0.0};
     const StreamSrc none{nullptr, 0, nullptr};
-    // the eligible cells of one tensor (edited: the board), band by band
-    auto count = [&](const u32 *g, bool edited) {
+    // the eligible cells of one tensor, band by band
+    auto count = [&](const u32 *g) {
         int n = 0;
 #pragma unroll 1
         for (int t = 0; t < NB; t++) {
             const int ru = (32 * t - 1) & (N - 1), rd = (32 * t + 32) & (N - 1);
-            u32 up = g[ru * RS], dn = g[rd * RS];
+            const u32 up = g[ru * RS], dn = g[rd * RS];
             u32 P[32];
             load_pairs_nt<RS>(g + 32 * t * RS, P);
             transpose32(P);
-            if (edited && ne > 0) {
-                up = edit_row(up, ru, ne, eidx, eval, lane);
-                dn = edit_row(dn, rd, ne, eidx, eval, lane);
-                (void)apply_edits(P, ne, eidx, eval, 32 * t, lane);
-            }
             GeoBand<SPAWN_COUNT> geo{lane, 32 * t, HaloView{up, dn}, none, 0, 0, 0, nullptr};
             u32 ch[2];
             rule_planes(P, ch, geo, sc, 0u);
@@ -443,8 +373,8 @@ k_stream_prologue128(Step128KArgs ka) {
     // a board or goals without spawners (spawn_flags, set at reset: no rule or action
     // creates one) draws nothing; nor do goals at their fixed point (planes_ok bit 2)
     const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);     // toggling powers can make one
-    const int nb = (spf & 1) ? count(gb, true) : 0;
-    const int ng = ((rec(V, R_POK) & 6) == 6 || !(spf & 2)) ? 0 : count(gg, false);
+    const int nb = (spf & 1) ? count(gb) : 0;
+    const int ng = ((rec(V, R_POK) & 6) == 6 || !(spf & 2)) ? 0 : count(gg);
     if (lane == 0) {
         w.counts[2 * b] = nb;
         w.counts[2 * b + 1] = ng;
@@ -466,6 +396,8 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
     const Step128KArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
     const dim3 grid((unsigned)st.B);
     if (fx.stream) {
+        const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
+        if (rca) return rca;
         hipLaunchKernelGGL(k_stream_prologue128, grid, dim3(64), 0, s, ka);
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
         const int rc = stream_offsets(st, fx, s);

@@ -109,12 +109,13 @@ struct SmallCells {
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 constexpr int kGroup = 8;
 
-__device__ __forceinline__ void stage_tensors(const uint16_t *const src[3], lds_u16 *const dst[3],
-                                              int HW, int W, int lane) {
+template <int NTEN = 3>
+__device__ __forceinline__ void stage_tensors(const uint16_t *const src[NTEN],
+                                              lds_u16 *const dst[NTEN], int HW, int W, int lane) {
     const int dy = 64 / W, dx = 64 - dy * W;
     int y = lane / W, x = lane - (lane / W) * W;
     for (int i0 = lane; i0 < HW; i0 += 64 * kGroup) {
-        uint32_t v[3][kGroup];
+        uint32_t v[NTEN][kGroup];
         int pos[kGroup];
 #pragma unroll
         for (int g = 0; g < kGroup; g++) {
@@ -122,7 +123,7 @@ __device__ __forceinline__ void stage_tensors(const uint16_t *const src[3], lds_
             pos[g] = -1;
             if (i < HW) {
 #pragma unroll
-                for (int t = 0; t < 3; t++) v[t][g] = src[t][i];
+                for (int t = 0; t < NTEN; t++) v[t][g] = src[t][i];
                 pos[g] = y * 64 + x + ((x == 0 && (W & 1)) ? 0x10000 : 0);
             }
             y += dy;
@@ -137,7 +138,7 @@ __device__ __forceinline__ void stage_tensors(const uint16_t *const src[3], lds_
             if (pos[g] >= 0) {
                 const int p = pos[g] & 0xFFFF;
 #pragma unroll
-                for (int t = 0; t < 3; t++) {
+                for (int t = 0; t < NTEN; t++) {
                     dst[t][p] = (uint16_t)v[t][g];
                     if (pos[g] >> 16) dst[t][p + W] = (uint16_t)v[t][g];    // column-0 copy
                 }
@@ -266,8 +267,8 @@ __device__ __forceinline__ void small_reset(const sl_env_state &st, const sl_lev
     }
 }
 
-// MODE: SPAWN_PHILOX, or SPAWN_STREAM (replay: k_stream_prologue_small has run the
-// action and sized the draws; the step reads act[b] and each tensor's first uniform
+// MODE: SPAWN_PHILOX, or SPAWN_STREAM (replay: k_env_action has run the action and
+// k_stream_prologue_small sized the draws; the step reads act[b] and each tensor's first uniform
 // from the scratch words)
 template <int MODE>
 __global__ void __launch_bounds__(64, SL_SMALL_MINW)
@@ -353,7 +354,7 @@ k_env_step_small(SmallKArgs ka) {
     RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
                rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     int act_reward = 0;
-    if (MODE == SPAWN_STREAM) {        // the prologue ran the action (no edits left)
+    if (MODE == SPAWN_STREAM) {        // k_env_action ran the action (no edits left)
         act_reward = (int)scratch_of(ka.scratch, st.B).act[b];
     } else {
         if (lane == 0) act_reward = act_core<64>(env, rec(V, R_ACT), H, W, ctp, ctc, ov);
@@ -899,11 +900,12 @@ k_env_step_seg4(SmallKArgs ka) {
     }
 }
 
-// Replay-mode prologue of env b (SL_RNG_STREAM), one wave: the action (state, its
-// cell edits into the board in HBM, its reward into scratch act[b]), then the eligible
-// cells of the acted-on board and of the goals (scratch counts[2b], [2b+1];
-// sl_exclusive_scan_i64 turns them into each tensor's first uniform).  The work of k_env_action
-// + k_env_count (sl_env.hip) on the bit-sliced rule.
+// Replay-mode count of env b (SL_RNG_STREAM), one wave, after k_env_action (one lane
+// per env) has applied the actions -- state and cell edits in HBM, rewards in scratch
+// act[] -- so the board staged here is the acted-on one: the eligible cells of the
+// board and of the goals (scratch counts[2b], [2b+1]; sl_exclusive_scan_i64 turns them
+// into each tensor's first uniform).  The work of k_env_count (sl_env.hip) on the
+// bit-sliced rule; a tensor without spawners is not read.
 __global__ void __launch_bounds__(64)
 k_stream_prologue_small(SmallKArgs ka) {
     const sl_env_state &st = ka.st;
@@ -911,52 +913,32 @@ k_stream_prologue_small(SmallKArgs ka) {
     const int lane = threadIdx.x;
     const int H = st.H, W = st.W, nl = (W + 1) >> 1;
     extern __shared__ __attribute__((aligned(16))) u32 dyn_stage[];
-    u32 *stage[3] = {dyn_stage, dyn_stage + H * 32, dyn_stage + 2 * H * 32};
+    u32 *stage[2] = {dyn_stage, dyn_stage + H * 32};
     const bool active = lane < nl;
     const int64_t off = b * (int64_t)H * W;
     const u32 V = load_record(st, ka.actions, b, lane);
-    {
-        const uint16_t *src[3] = {st.board + off, st.goals + off, st.start_board + off};
-        lds_u16 *dst[3] = {(lds_u16 *)stage[0], (lds_u16 *)stage[1], (lds_u16 *)stage[2]};
-        stage_tensors(src, dst, H * W, W, lane);
-    }
-    wait_lgkm();
-    OverlayT<SmallCells> ov;
-    ov.src.buf = (lds_u32 *)stage[0];
-    ov.n = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        ov.idx[k] = 0;
-        ov.val[k] = 0;
-    }
-    RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
-               rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     const Scratch w = scratch_of(ka.scratch, st.B);
-    if (lane == 0) {
-        w.act[b] = act_core<64>(env, rec(V, R_ACT), H, W, ka.ctp, ka.ctc, ov);
-        lds_u16 *cells = (lds_u16 *)stage[0];
-        for (int k = 0; k < ov.n; k++) {
-            const int i = ov.idx[k], y = i >> 6, x = i & 63;
-            cells[i] = (uint16_t)ov.val[k];
-            if ((W & 1) && x == 0) cells[i + W] = (uint16_t)ov.val[k];
-            st.board[off + y * W + x] = (uint16_t)ov.val[k];
-        }
-    }
-    SpawnCtx sc{0u, 0u, 0ull, 0.0};
-    int n[2] = {0, 0};
     // no spawner in the tensor (spawn_flags, set at reset; toggling powers can make
     // one on the board): no draws
     const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);
+    int n[2] = {0, 0};
+    if (spf & 3) {
+        const uint16_t *src[2] = {st.board + off, st.goals + off};
+        lds_u16 *dst[2] = {(lds_u16 *)stage[0], (lds_u16 *)stage[1]};
+        stage_tensors<2>(src, dst, H * W, W, lane);
+        wait_lgkm();
+        SpawnCtx sc{0u, 0u, 0ull, 0.0};
 #pragma unroll 1
-    for (int t = 0; t < 2; t++) {
-        if (!((spf >> t) & 1)) continue;
-        u32 P[32];
-        lds_rows((const lds_u16 *)stage[t], H, active, lane, P);
-        transpose32(P);
-        GeoSmall<SPAWN_COUNT> geo = small_geo<SPAWN_COUNT>(lane, H, W);
-        u32 ch[2];
-        rule_planes(P, ch, geo, sc, (u32)t);
-        n[t] = wave_total(geo.count);
+        for (int t = 0; t < 2; t++) {
+            if (!((spf >> t) & 1)) continue;
+            u32 P[32];
+            lds_rows((const lds_u16 *)stage[t], H, active, lane, P);
+            transpose32(P);
+            GeoSmall<SPAWN_COUNT> geo = small_geo<SPAWN_COUNT>(lane, H, W);
+            u32 ch[2];
+            rule_planes(P, ch, geo, sc, (u32)t);
+            n[t] = wave_total(geo.count);
+        }
     }
     if (lane == 0) {
         w.counts[2 * b] = n[0];
@@ -989,7 +971,10 @@ int launch_step_small(const sl_env_state &st, const StepArgs &a, const FastExtra
     const dim3 grid4((unsigned)((st.B + 3) / 4));
     const size_t lds4 = (size_t)3 * seg_stride(st.H, st.W) * sizeof(uint16_t);
     if (fx.stream) {
-        hipLaunchKernelGGL(k_stream_prologue_small, grid, dim3(64), lds, s, ka);
+        const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
+        if (rca) return rca;
+        hipLaunchKernelGGL(k_stream_prologue_small, grid, dim3(64), (size_t)2 * st.H * 32 * sizeof(uint32_t),
+                           s, ka);
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
         const int rc = stream_offsets(st, fx, s);
         if (rc) return rc;
