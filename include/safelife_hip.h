@@ -57,8 +57,9 @@ extern "C" {
                                counter (block, env, step, tensor), 32-bit words */
 
 #define SL_KERNEL_AUTO 0     /* bit-sliced kernels for 64x64, 128x128 and boards
-                                up to 32x64 (both RNG modes; replay adds a
-                                prologue kernel + a scan per step), the generic
+                                up to 32x64 (both RNG modes; replay adds an
+                                action kernel, a count kernel and a scan per
+                                step), the generic
                                 kernel for other shapes                      */
 #define SL_KERNEL_GENERIC 1  /* LDS-staged per-cell kernel, any shape        */
 #define SL_KERNEL_FAST 2     /* require the fast kernel (error if none)      */
