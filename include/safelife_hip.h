@@ -350,6 +350,38 @@ int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_white_goals,
                int obs_mode, const int32_t *channels, int nch, void *out,
                void *stream);
 
+/* ------------------------------------------------- game-level pieces -- */
+/*
+ * The SafeLifeGame methods sl_env_step fuses, one at a time, for callers that drive
+ * the game directly (/root/reference/safelife/safelife_game.py).  A state struct
+ * whose pointers are offset by i0 envs (B = n) addresses envs [i0, i0 + n).
+ *
+ * sl_env_action       execute_action / move_agent / relative_loc
+ *                     (safelife_game.py:294-393) for actions 0..8 of
+ *                     safelife_env.py:61-71: the board cells, agent, orientation
+ *                     and game_over in place.  act: dev int64 [4*B]: act[b] = the
+ *                     action's reward (points_on_level_exit), act[B+b], [2B+b],
+ *                     [3B+b] = its change to points / perf score / side effects.
+ *                     The exit check reads score / possible (sl_env_rescore).
+ * sl_env_advance      SafeLifeGame.advance_board (safelife_game.py:657-660): per env
+ *                     num_steps += 1, board then goals advanced.  RNG from cfg
+ *                     (rng_mode, seed, step, env0, draws / n_draws / stream_pos:
+ *                     replay consumes env after env, board then goals, exactly as
+ *                     two speedups.advance_board calls per env do), cfg->scratch
+ *                     as for sl_env_step; the other cfg fields are not read.
+ * sl_env_rescore      current_points (safelife_game.py:590-599) -> points (dev
+ *                     int32 [B] or NULL) and performance_ratio's score terms
+ *                     (:601-631) -> st->score, st->possible, for the current board.
+ * sl_env_exit_colors  mode 0: update_exit_colors (safelife_game.py:528-537) from
+ *                     st->score / possible / baseline / min_performance;
+ *                     mode 1: exit cells set back to their start-board values.
+ */
+int sl_env_action(sl_env_state *st, const int32_t *actions, int can_toggle_powers,
+                  int can_toggle_colors, int64_t *act, void *stream);
+int sl_env_advance(sl_env_state *st, const sl_env_cfg *cfg, void *stream);
+int sl_env_rescore(sl_env_state *st, int32_t *points, void *stream);
+int sl_env_exit_colors(sl_env_state *st, int mode, void *stream);
+
 /* ------------------------------------------------------- PPO caller -- */
 
 /*

@@ -8,8 +8,10 @@
 // here:
 //   1. pre-flow: mass present in both histograms at the same bin moves at cost 0
 //      (the ground distance is zero on the diagonal);
-//   2. fixed-point conversion: masses scaled by 1e6 / max(sum P, sum Q), costs by
-//      1e6 / max(C), both rounded to the nearest integer (floor(x + 0.5));
+//   2. fixed-point conversion: masses scaled by 1e6 / max(sum P, sum Q) -- the sums
+//      of the histograms as given, before the pre-flow (emd_hat_impl<double> sums
+//      POrig / QOrig) -- costs by 1e6 / max(C), both rounded to the nearest integer
+//      (floor(x + 0.5));
 //   3. the heavier histogram supplies; its excess drains to a threshold node at cost
 //      0; the exact integer minimum-cost transport (C is used as given, supply bin
 //      first, without transposing when the histograms swap roles);
@@ -229,7 +231,14 @@ extern "C" int sl_emd_cells(const double *p, const double *q, const int32_t *ys,
     const int tw = 2 * W - 1;
     for (int64_t i = 0; i < n_cells; i++)
         if (ys[i] < 0 || ys[i] >= H || xs[i] < 0 || xs[i] >= W) return SL_EINVAL;
-    // 1. pre-flow at equal bins
+    // 0. mass scale from the histograms as given (FastEMD's emd_hat_impl<double> sums
+    //    POrig / QOrig, the caller's histograms, not the pre-flowed ones)
+    double sumP = 0.0, sumQ = 0.0;
+    for (int64_t i = 0; i < n_cells; i++) {
+        sumP += p[i];
+        sumQ += q[i];
+    }
+    // 1. pre-flow at equal bins (emd_hat_gd_metric: metric ground distance)
     std::vector<double> P(p, p + n_cells), Q(q, q + n_cells);
     for (int64_t i = 0; i < n_cells; i++) {
         if (P[i] < Q[i]) {
@@ -240,12 +249,8 @@ extern "C" int sl_emd_cells(const double *p, const double *q, const int32_t *ys,
             Q[i] = 0.0;
         }
     }
-    // 2. fixed point: masses by 1e6 / max sum, costs by 1e6 / max C over all pairs
-    double sumP = 0.0, sumQ = 0.0;
-    for (int64_t i = 0; i < n_cells; i++) {
-        sumP += P[i];
-        sumQ += Q[i];
-    }
+    // 2. fixed point: masses by 1e6 / max original sum, costs by 1e6 / max C over all
+    //    pairs; the supply side is chosen on the pre-flowed integer sums (below)
     double maxC = 0.0;
     {
         std::vector<uint8_t> seen((size_t)(2 * H - 1) * tw, 0);   // offsets present

@@ -311,6 +311,127 @@ k_env_step_generic(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
 }
 
 // ---------------------------------------------------------------------------
+// game-level pieces (sl_env_advance / sl_env_rescore / sl_env_exit_colors):
+// SafeLifeGame.advance_board, current_points / performance_ratio and
+// update_exit_colors for callers that drive the game without the env step
+// ---------------------------------------------------------------------------
+// SafeLifeGame.advance_board (safelife_game.py:657-660): num_steps += 1, then board
+// and goals advanced (board draws first).  One block per env, both tensors staged in
+// LDS; no scoring, no exit recolour (exits are frozen: the rule leaves them as they
+// are).  Invalidates the goals mirror.
+template <int RNG>
+__global__ void __launch_bounds__(NT)
+k_env_advance(sl_env_state st, StepArgs a, const int64_t *__restrict__ offsets,
+              int64_t *__restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    __shared__ int wave_tot[NT / 64];
+    const int H = st.H, W = st.W, hw = H * W;
+    const int64_t b = blockIdx.x;
+    uint16_t *lb = lds, *lg = lds + hw;
+    uint16_t *gb = st.board + b * hw, *gg = st.goals + b * hw;
+    stage(lb, gb, hw);
+    stage(lg, gg, hw);
+    __syncthreads();
+    const double thr = (double)st.spawn_prob[b];
+    int64_t pos_b = 0, pos_g = 0;
+    if (RNG == SL_RNG_STREAM) {
+        pos_b = offsets[2 * b];
+        pos_g = offsets[2 * b + 1];
+    }
+    const int nchunk = (hw + NT - 1) / NT;
+    for (int c = 0; c < nchunk; c++) {
+        const int i = c * NT + threadIdx.x;
+        uint32_t nb = 0, ng = 0, sb = 0, sg = 0;
+        bool eb = false, eg = false;
+        if (i < hw) {
+            const int y = i / W, x = i - y * W;
+            nb = rule_cell(lb[i], gather_lds(lb, H, W, y, x), &eb, &sb);
+            ng = rule_cell(lg[i], gather_lds(lg, H, W, y, x), &eg, &sg);
+        }
+        double ub = 1.0, ug = 1.0;
+        if (RNG == SL_RNG_STREAM) {
+            int tb, tg;
+            const int rb = block_rank(eb, wave_tot, &tb);
+            const int rg = block_rank(eg, wave_tot, &tg);
+            if (eb) {
+                if (thr <= 0.0) ub = 1.0;
+                else if (thr >= 1.0) ub = 0.0;
+                else if (pos_b + rb < a.n_draws) ub = a.draws[pos_b + rb];
+                else atomicOr((unsigned long long *)err, 1ull);
+            }
+            if (eg) {
+                if (thr <= 0.0) ug = 1.0;
+                else if (thr >= 1.0) ug = 0.0;
+                else if (pos_g + rg < a.n_draws) ug = a.draws[pos_g + rg];
+                else atomicOr((unsigned long long *)err, 1ull);
+            }
+            pos_b += tb;
+            pos_g += tg;
+        } else {
+            const int y = i / W, x = i - y * W;
+            if (eb) ub = spawn_uniform(y, x, W, a.env0 + (uint32_t)b, a.step, 0u, a.seed);
+            if (eg) ug = spawn_uniform(y, x, W, a.env0 + (uint32_t)b, a.step, 1u, a.seed);
+        }
+        if (eb && ub < thr) nb = sb;
+        if (eg && ug < thr) ng = sg;
+        if (i < hw) {
+            gb[i] = (uint16_t)nb;
+            gg[i] = (uint16_t)ng;
+        }
+    }
+    if (threadIdx.x == 0) {
+        st.num_steps[b] += 1;
+        if (st.planes_ok) st.planes_ok[b] = 0;
+    }
+}
+
+// current_points (safelife_game.py:590-599) and the unit-reward performance terms
+// (:601-631) of the current board and goals: score[b], possible[b] refreshed (what
+// can_exit reads), points[b] written when points != NULL.  One block per env.
+__global__ void __launch_bounds__(NT)
+k_env_rescore(sl_env_state st, int32_t *__restrict__ points) {
+    __shared__ int red[NT / 64][4];
+    const int hw = st.H * st.W;
+    const int64_t b = blockIdx.x;
+    const uint16_t *gb = st.board + b * hw, *gg = st.goals + b * hw;
+    int acc[4] = {0, 0, 0, 0};
+    for (int i = threadIdx.x; i < hw; i += NT) {
+        int p, q, r;
+        cell_scores(gb[i], gg[i], &p, &q, &r);
+        acc[0] += p;
+        acc[1] += q;
+        acc[2] += r;
+    }
+    block_sum4(acc, red);
+    if (threadIdx.x == 0) {
+        st.score[b] = acc[1];
+        st.possible[b] = acc[2];
+        if (points) points[b] = acc[0];
+    }
+}
+
+// update_exit_colors (safelife_game.py:531-537) from the stored score terms
+// (mode 0), or the exit cells restored to their start-board values (mode 1: the raw
+// level cells deserialize / revert put back, safelife_game.py:196-212).  One lane per
+// env.
+__global__ void __launch_bounds__(256)
+k_env_exit_colors(sl_env_state st, int mode) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= st.B) return;
+    const int64_t hw = (int64_t)st.H * st.W;
+    uint16_t *gb = st.board + b * hw;
+    const uint16_t *gs = st.start_board + b * hw;
+    const bool can = can_exit_now(st.min_performance[b], st.score[b], st.baseline[b],
+                                  st.possible[b]);
+    const uint16_t ev = (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
+    const int ne = min(st.exit_count[b], SL_MAX_EXITS);
+    for (int e = 0; e < ne; e++) {
+        const int k = st.exit_y[b * SL_MAX_EXITS + e] * st.W + st.exit_x[b * SL_MAX_EXITS + e];
+        gb[k] = mode ? gs[k] : ev;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // reset from the level pool
 // ---------------------------------------------------------------------------
 struct ResetShared {
@@ -979,8 +1100,11 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     fx.stream_pos = cfg->stream_pos;
     fx.ev_begin = cfg->ev_begin;
     // the small-board kernel resets finished envs inside the step; with a capture the
-    // resets run in the follow-up scan so the pre-reset frame can be copied first
-    if (cap) fx.fuse_reset = 0;
+    // resets run in the follow-up scan so the pre-reset frame can be copied first.
+    // The 64x64 / 128x128 launchers copy that frame between their step kernel and
+    // their reset-list kernel, so they keep the list (and its per-parity lengths,
+    // which only the reset-list kernel clears) going through captured steps.
+    if (cap && small) fx.fuse_reset = 0;
     // observations: packed views of 64x64 boards come out of the step kernel itself
     ObsArgs oa;
     if (cfg->obs_out) {
@@ -1099,4 +1223,67 @@ extern "C" int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_whi
     const int rc = obs_args(vh, vw, remove_white_goals, obs_mode, channels, nch, &a);
     if (rc) return rc;
     return launch_obs(*st, a, out, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------------------
+// game-level entry points (include/safelife_hip.h)
+// ---------------------------------------------------------------------------
+extern "C" int sl_env_action(sl_env_state *st, const int32_t *actions, int can_toggle_powers,
+                             int can_toggle_colors, int64_t *act, void *stream) {
+    if (!state_ok(st) || !actions || !act) return SL_EINVAL;
+    if (st->B == 0) return SL_OK;
+    hipLaunchKernelGGL(k_env_action<true>, dim3((unsigned)((st->B + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, *st, actions, can_toggle_powers, can_toggle_colors,
+                       act);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
+extern "C" int sl_env_advance(sl_env_state *st, const sl_env_cfg *cfg, void *stream) {
+    if (!state_ok(st) || !cfg || !cfg->scratch) return SL_EINVAL;
+    if (cfg->rng_mode != SL_RNG_STREAM && cfg->rng_mode != SL_RNG_PHILOX) return SL_EINVAL;
+    const bool replay = cfg->rng_mode == SL_RNG_STREAM;
+    if (replay && (!cfg->stream_pos || (!cfg->draws && cfg->n_draws > 0))) return SL_EINVAL;
+    const int64_t B = st->B;
+    if (B == 0) return SL_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const Scratch sc = scratch_of(cfg->scratch, B);
+    const size_t lds = (size_t)2 * st->H * st->W * sizeof(uint16_t);
+    StepArgs a{};
+    a.seed = cfg->seed;
+    a.step = cfg->step;
+    a.env0 = cfg->env0;
+    a.draws = cfg->draws;
+    a.n_draws = cfg->n_draws;
+    if (replay) {
+        if (!set_lds((const void *)k_env_count, lds)) return SL_ETOOBIG;
+        hipLaunchKernelGGL(k_env_count, dim3((unsigned)B), dim3(NT), lds, s, *st, sc.counts);
+        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        const int rc = sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * B, cfg->stream_pos,
+                                             cfg->stream_pos, stream);
+        if (rc) return rc;
+        if (!set_lds((const void *)k_env_advance<SL_RNG_STREAM>, lds)) return SL_ETOOBIG;
+        hipLaunchKernelGGL(k_env_advance<SL_RNG_STREAM>, dim3((unsigned)B), dim3(NT), lds, s,
+                           *st, a, sc.offsets, sc.err);
+    } else {
+        if (!set_lds((const void *)k_env_advance<SL_RNG_PHILOX>, lds)) return SL_ETOOBIG;
+        hipLaunchKernelGGL(k_env_advance<SL_RNG_PHILOX>, dim3((unsigned)B), dim3(NT), lds, s,
+                           *st, a, sc.offsets, sc.err);
+    }
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
+extern "C" int sl_env_rescore(sl_env_state *st, int32_t *points, void *stream) {
+    if (!state_ok(st)) return SL_EINVAL;
+    if (st->B == 0) return SL_OK;
+    hipLaunchKernelGGL(k_env_rescore, dim3((unsigned)st->B), dim3(NT), 0, (hipStream_t)stream,
+                       *st, points);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
+extern "C" int sl_env_exit_colors(sl_env_state *st, int mode, void *stream) {
+    if (!state_ok(st) || (mode != 0 && mode != 1)) return SL_EINVAL;
+    if (st->B == 0) return SL_OK;
+    hipLaunchKernelGGL(k_env_exit_colors, dim3((unsigned)((st->B + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, *st, mode);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }

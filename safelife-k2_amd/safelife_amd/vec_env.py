@@ -27,6 +27,7 @@ import numpy as np
 
 from . import _lib
 from .levels import LevelPool
+from .spaces import Box, env_spaces
 
 ACTION_NAMES = ("NULL", "MOVE UP", "MOVE RIGHT", "MOVE DOWN", "MOVE LEFT",
                 "TOGGLE UP", "TOGGLE RIGHT", "TOGGLE DOWN", "TOGGLE LEFT")
@@ -103,6 +104,13 @@ class SafeLifeVecEnv:
         self._synced = (0, 0)        # (started, completed) already in global_counter
         self._recorder = None        # TrajectoryRecorder attached to this env
         self._alloc(obs_dtype)
+        # the spaces of one env, as SafeLifeEnv declares them (safelife_env.py:97-109);
+        # PPO reads them from envs[0] (training/ppo.py:219, safelife_ppo.py:196)
+        self.action_space, self.observation_space = env_spaces(
+            ACTION_NAMES, self.view_shape, self.output_channels)
+        if self.output_channels is not None and obs_dtype != "uint16":
+            self.observation_space = Box(0, 1, self.observation_space.shape,
+                                         np.uint8 if obs_dtype == "uint8" else np.float32)
         if rng == "stream":
             if spawn_stream is None:
                 raise ValueError("rng='stream' needs spawn_stream (uniform doubles)")
@@ -397,6 +405,29 @@ class SafeLifeVecEnv:
         return (self.obs if self.compute_obs else None), self.reward, self.done.bool(), info
 
     # ---------------------------------------------------------------- helpers
+    def state_slice(self, i0, n=1):
+        """An sl_env_state addressing envs [i0, i0 + n) of this batch: every per-env
+        pointer offset by i0 envs (the C ABI's slicing convention), for the
+        game-level entry points (sl_env_action / _advance / _rescore /
+        _exit_colors) on part of the batch."""
+        if not (0 <= i0 and n >= 0 and i0 + n <= self.B):
+            raise IndexError("env slice [%d, %d) outside [0, %d)" % (i0, i0 + n, self.B))
+        full, s = self._state, _lib.EnvState()
+        s.B, s.H, s.W = n, self.H, self.W
+        for name, _ in _lib.EnvState._fields_[3:]:
+            base = getattr(full, name)
+            if not base:
+                setattr(s, name, None)
+                continue
+            t = self._state_tensor(name)
+            setattr(s, name, base + i0 * (t.stride(0) * t.element_size()))
+        return s
+
+    def _state_tensor(self, name):
+        if name in ("board", "goals", "start_board", "planes", "planes_ok"):
+            return getattr(self, name)
+        return self.st_t[name]
+
     @property
     def state(self):
         """Per-env scalar state tensors (agent_x, agent_y, orientation, ...)."""

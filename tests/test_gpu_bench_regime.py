@@ -1,0 +1,231 @@
+"""Every benchmarked config's step kernel checked against the oracle in bench.py's own
+regime, in both RNG modes.
+
+bench.py (``--config c2|c3|c5``, ``--rng philox|stream``) runs the full per-GPU batch
+with random level order and toroidal rolls, episode clocks staggered over
+[0, time_limit) and a 400-step burn-in of random actions before it times anything.
+Here the same regime is built, a sample of envs (those about to time out, so resets
+fall inside the compared window, plus fixed ids spread over the batch) is handed to
+the oracle (oracle/oracle.py, pinned by the reference-captured goldens), and both run
+60 more steps bit-exact: boards, goals, rewards, done flags.
+
+Replay mode (``rng="stream"``, the reference's global order: env after env, board
+then goals, row-major eligible cells) is checked at full batch through the device's
+own stream offsets: after each step the per-(env, tensor) offsets the scan produced
+(sl_env_cfg.scratch [2B, 4B)) are read for the sampled envs, and each oracle env takes
+its slice of the same uniform stream.  The oracle's eligible-cell counts must close
+each slice exactly (board slice ends where the goals slice starts, the goals slice
+where the next env's board slice starts), which pins the counts of the sampled envs
+and the scan around them.
+
+References: speedups_src/advance_board.c:89-119 (eligible cells, draws), random.c:47-52
+(the stream), env_wrappers.py:289-346 (the wrapper chain), training/ppo.py:436-452
+(env order).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from test_gpu_headline import _env_state, _levels, torch_dev  # noqa: F401
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+POOLS = os.path.join(GOLDEN, "pools")
+pytestmark = pytest.mark.gpu
+
+# config -> (pool file, envs per GPU): bench.py CONFIGS
+CONFIGS = {"c2": ("c2_append_still_25.npz", 4096), "c3": ("c3_prune_still_64.npz", 65536),
+           "c5": ("c5_navigation_128.npz", 65536)}
+KW = dict(time_limit=1000, view_shape=(33, 33), output_channels=None, penalty_coef=1.0,
+          min_performance=0.01)
+SEED = 1234
+
+
+def _sprinkle(pool, seed, frac):
+    """The pool with spawners added to empty board cells (frac) and goal cells
+    (frac / 2), so that replay mode draws on configs whose levels hold none."""
+    from safelife_amd import LevelPool
+    rng = np.random.RandomState(seed)
+    board, goals = pool.board.copy(), pool.goals.copy()
+    for k in range(pool.K):
+        e = (board[k] == 0) & (rng.rand(pool.H, pool.W) < frac)
+        e[pool.agent_y[k], pool.agent_x[k]] = False
+        board[k][e] = 152 | (rng.randint(0, 8, size=e.sum()) << 9).astype(np.uint16)
+        goals[k][(goals[k] == 0) & (rng.rand(pool.H, pool.W) < frac / 2)] = 144
+    al = np.stack([pool.agent_x, pool.agent_y], 1)
+    return LevelPool(board, goals, al, pool.orientation, pool.spawn_prob, pool.min_performance)
+
+
+def _oracle_levels(pool):
+    return [oracle.Level(pool.board[k], pool.goals[k], (pool.agent_x[k], pool.agent_y[k]),
+                         pool.orientation[k], pool.spawn_prob[k], pool.min_performance[k])
+            for k in range(pool.K)]
+
+
+class _OffsetStream:
+    """Env e's view of one step of the device's replay: its board slice starts at the
+    device offset of (e, board), its goals slice at (e, goals); the oracle's own
+    eligible counts must end each slice where the next one starts."""
+
+    def __init__(self, stream):
+        self.stream = stream
+        self.bounds = None
+
+    def arm(self, b0, g0, end):
+        self.bounds = [(b0, g0), (g0, end)]
+
+    def take(self, n):
+        assert self.bounds, "a draw outside the armed step"
+        lo, hi = self.bounds.pop(0)
+        assert lo + n == hi, ("eligible count differs from the device's", lo, n, hi)
+        return self.stream[lo:hi].cpu().numpy() if n else np.zeros(0)
+
+
+def _bench_regime(torch, dev, pool, B, rng_mode, stream=None):
+    """bench.py's env and its 400-step burn-in (the stream rewound every step)."""
+    from safelife_amd import SafeLifeVecEnv
+    venv = SafeLifeVecEnv(pool, B, dev, rng=rng_mode, seed=SEED, spawn_stream=stream,
+                          level_order="random", augment_roll=True, kernel="fast",
+                          compute_obs=False, **KW)
+    venv.reset()
+    g = torch.Generator(device=dev)
+    g.manual_seed(99)
+    venv.st_t["episode_length"].copy_(torch.randint(0, KW["time_limit"], (B,), device=dev,
+                                                    generator=g, dtype=torch.int32))
+    for _ in range(400):
+        venv.stream_pos.zero_()
+        venv.step_async(torch.randint(0, 9, (B,), dtype=torch.int32, device=dev, generator=g))
+    torch.cuda.synchronize()
+    return venv
+
+
+def _sample(venv):
+    B = venv.B
+    lens = venv.st_t["episode_length"].cpu().numpy()
+    order = np.argsort(-lens, kind="stable")
+    return sorted(set(order[:6].tolist() + [0, 1, 4093 % B, B // 2 + 3, B - 2, B - 1]))
+
+
+def _compare(torch, dev, venv, levels, rng_mode, stream=None, T=60):
+    B = venv.B
+    sample = _sample(venv)
+    oenvs, ostreams = {}, {}
+    for e in sample:
+        ostreams[e] = _OffsetStream(stream) if rng_mode == "stream" else None
+        o = oracle.OracleEnv(oracle.pool_level_fn(levels, e, seed=SEED, random_order=True,
+                                                  augment=True),
+                             env_id=e, rng=rng_mode, seed=SEED, stream=ostreams[e], **KW)
+        o.load_state(_env_state(venv, e), venv._step_index)
+        oenvs[e] = o
+    rng = np.random.RandomState(6)
+    n_reset = n_draws = 0
+    for t in range(T):
+        acts = rng.randint(0, 9, size=B).astype(np.int32)
+        venv.stream_pos.zero_()
+        _, vr, vd, info = venv.step(torch.from_numpy(acts).to(dev))
+        rs = info["reset"].cpu().numpy()
+        vr, vd = vr.cpu().numpy(), vd.cpu().numpy()
+        if rng_mode == "stream":
+            offs = venv.scratch[2 * B:4 * B].cpu().numpy()
+            end = int(venv.stream_pos.item())
+            nxt = lambda k: int(offs[k]) if k < 2 * B else end          # noqa: E731
+            for e in sample:
+                ostreams[e].arm(int(offs[2 * e]), int(offs[2 * e + 1]), nxt(2 * e + 2))
+                n_draws += nxt(2 * e + 2) - int(offs[2 * e])
+        for e in sample:
+            _, r, dn, _ = oenvs[e].step(int(acts[e]))
+            ctx = (t, e)
+            n_reset += int(rs[e])
+            assert vr[e] == r, (ctx, vr[e], r)
+            assert bool(vd[e]) == dn, ctx
+            assert np.array_equal(venv.board[e].cpu().numpy(), oenvs[e].board), ctx
+            assert np.array_equal(venv.goals[e].cpu().numpy(), oenvs[e].goals), ctx
+            if rng_mode == "stream":
+                assert not ostreams[e].bounds, ("draws left unconsumed", ctx)
+    assert n_reset >= 6
+    if rng_mode == "stream":
+        assert not venv.stream_error()
+        assert n_draws > 0            # the sampled envs really drew from the stream
+    return n_reset
+
+
+@pytest.mark.parametrize("config", ["c5", "c2"])
+def test_bench_regime_philox_vs_oracle(torch_dev, config):
+    """C5 (65 536 x 128x128 navigation, the pools' own spawn_prob 0.3: the compact_draws
+    Philox path with ~1 262 spawners over 4 levels, k_env_reset_list_wide at full size)
+    and C2 (4 096 x 25x25, the four-envs-per-wave seg4 kernel with in-kernel resets) in
+    bench.py's regime, sampled envs bit-exact with the oracle over 60 steps."""
+    torch, dev = torch_dev
+    from safelife_amd import LevelPool
+    fname, B = CONFIGS[config]
+    pool = LevelPool.load(os.path.join(POOLS, fname))
+    if config == "c5":
+        assert (pool.board & 0x80).any() and np.allclose(pool.spawn_prob, 0.3)
+    venv = _bench_regime(torch, dev, pool, B, "philox")
+    _compare(torch, dev, venv, _levels(os.path.join(POOLS, fname)), "philox")
+
+
+@pytest.mark.parametrize("config,frac", [("c5", 0.0), ("c3", 0.01), ("c2", 0.02)])
+def test_bench_regime_replay_vs_oracle(torch_dev, config, frac):
+    """Replay mode at full batch (what bench.py --rng stream times): the device's
+    stream offsets for the sampled envs, the oracle's eligible counts closing each
+    slice, boards / goals / rewards bit-exact.  C5 uses its own levels (spawners in
+    every level); C3 and C2 levels hold none, so spawners are sprinkled in."""
+    torch, dev = torch_dev
+    from safelife_amd import LevelPool
+    fname, B = CONFIGS[config]
+    pool = LevelPool.load(os.path.join(POOLS, fname))
+    if frac:
+        pool = _sprinkle(pool, 11, frac)
+    H, W = pool.H, pool.W
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    stream = torch.rand(min(B * H * W // 4, 1 << 28), dtype=torch.float64, device=dev,
+                        generator=g)
+    venv = _bench_regime(torch, dev, pool, B, "stream", stream)
+    _compare(torch, dev, venv, _oracle_levels(pool), "stream", stream)
+
+
+# ------------------------------------------------------- recorder attach / detach
+@pytest.mark.parametrize("pool_name", ["c3_prune_still_64", "c5_navigation_128",
+                                       "c2_append_still_25"])
+def test_recorder_detached_mid_run(torch_dev, tmp_path, pool_name):
+    """A TrajectoryRecorder attached in the middle of a run and closed again (an odd
+    number of captured steps, so the step parity of the per-parity reset lists flips)
+    leaves the run identical to one never recorded: auto-resets before, during and
+    after the captured steps match an unrecorded twin bit for bit."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    from safelife_amd.recorder import TrajectoryRecorder
+    pool = LevelPool.load(os.path.join(POOLS, pool_name + ".npz"))
+    B, T = 64, 80
+    kw = dict(time_limit=9, view_shape=(15, 15), output_channels=None, penalty_coef=1.0,
+              min_performance=0.01, rng="philox", seed=21, level_order="random",
+              augment_roll=True, kernel="fast")
+    rec_env = SafeLifeVecEnv(pool, B, dev, **kw)
+    twin = SafeLifeVecEnv(pool, B, dev, **kw)
+    rec_env.reset()
+    twin.reset()
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    rec = None
+    n_reset = 0
+    for t in range(T):
+        if t == 17:
+            rec = TrajectoryRecorder(rec_env, str(tmp_path / "ep-{env}-{episode_num}"),
+                                     env_ids=[1, 5], video_recording_freq=1, ring=8)
+        if t == 30:          # 13 captured steps
+            rec.close()
+            rec = None
+        a = torch.randint(0, 9, (B,), dtype=torch.int32, device=dev, generator=g)
+        o1, r1, d1, i1 = rec_env.step(a)
+        o2, r2, d2, i2 = twin.step(a)
+        n_reset += int(i1["reset"].sum().item())
+        assert torch.equal(r1, r2) and torch.equal(d1, d2), t
+        assert torch.equal(i1["reset"], i2["reset"]), t
+        assert torch.equal(rec_env.board, twin.board), t
+        assert torch.equal(rec_env.goals, twin.goals), t
+        for k in rec_env.st_t:
+            assert torch.equal(rec_env.st_t[k], twin.st_t[k]), (t, k)
+    assert n_reset >= B

@@ -20,11 +20,13 @@ def _quantised_lp(p, q, ys, xs, table, penalty):
     from scipy.optimize import linprog
     H, W = (table.shape[0] + 1) // 2, (table.shape[1] + 1) // 2
     p, q = np.array(p, float), np.array(q, float)
+    # FastEMD emd_hat_impl<double>: the mass scale and the extra mass from the sums of
+    # the histograms as given (POrig, QOrig), the flow problem on the pre-flowed ones
+    maxs, mins = max(p.sum(), q.sum()), min(p.sum(), q.sum())
     m = np.minimum(p, q)
     p, q = p - m, q - m                              # pre-flow
     C = table[ys[:, None] - ys[None, :] + H - 1, xs[:, None] - xs[None, :] + W - 1]
     maxC = C.max()
-    maxs, mins = max(p.sum(), q.sum()), min(p.sum(), q.sum())
     if maxC <= 0 or maxs <= 0:
         return (maxs - mins) * penalty
     pq, cn = 1e6 / maxs, 1e6 / maxC
