@@ -8,8 +8,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("SAFELIFE_HIP_LIB") or os.path.join(_HERE, "_native",
-                                                              "libsafelife_hip.so")
+_DEFAULT_LIB = os.path.join(_HERE, "_native", "libsafelife_hip.so")
+LIB_PATH = os.environ.get("SAFELIFE_HIP_LIB") or _DEFAULT_LIB
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 SL_OK, SL_EINVAL, SL_EHIP, SL_ETOOBIG = 0, -1, -2, -3
@@ -119,18 +119,22 @@ def lib():
     L.sl_gae.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, i64, f64, vp, vp, vp]
     L.sl_emd_cells.argtypes = [vp, vp, vp, vp, i64, vp, ctypes.c_int, ctypes.c_int, f64,
                                ctypes.POINTER(f64)]
-    L.sl_env_action.argtypes = [ctypes.POINTER(EnvState), vp, ctypes.c_int, ctypes.c_int, vp, vp]
-    L.sl_env_advance.argtypes = [ctypes.POINTER(EnvState), ctypes.POINTER(EnvCfg), vp]
-    L.sl_env_rescore.argtypes = [ctypes.POINTER(EnvState), vp, vp]
-    L.sl_env_exit_colors.argtypes = [ctypes.POINTER(EnvState), ctypes.c_int, vp]
+    game = {"sl_env_action": [ctypes.POINTER(EnvState), vp, ctypes.c_int, ctypes.c_int, vp, vp],
+            "sl_env_advance": [ctypes.POINTER(EnvState), ctypes.POINTER(EnvCfg), vp],
+            "sl_env_rescore": [ctypes.POINTER(EnvState), vp, vp],
+            "sl_env_exit_colors": [ctypes.POINTER(EnvState), ctypes.c_int, vp]}
+    for name, args in game.items():
+        # (an A/B build of an older revision, SAFELIFE_HIP_LIB, may lack these)
+        if hasattr(L, name) or LIB_PATH == _DEFAULT_LIB:
+            getattr(L, name).argtypes = args
+            getattr(L, name).restype = ctypes.c_int
     L.sl_event_create.argtypes = [ctypes.POINTER(vp)]
     L.sl_event_destroy.argtypes = [vp]
     L.sl_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(f32)]
     for name in ("sl_event_create", "sl_event_destroy", "sl_event_elapsed_ms", "sl_device_arch", "sl_advance", "sl_count_eligible", "sl_exclusive_scan_i64",
                  "sl_env_step", "sl_env_reset", "sl_env_obs", "sl_level_pool_prepare",
                  "sl_side_effect_workspace", "sl_side_effect_densities",
-                 "sl_sample_actions", "sl_gae", "sl_emd_cells", "sl_copy16",
-                 "sl_env_action", "sl_env_advance", "sl_env_rescore", "sl_env_exit_colors"):
+                 "sl_sample_actions", "sl_gae", "sl_emd_cells", "sl_copy16"):
         getattr(L, name).restype = ctypes.c_int
     _lib = L
     return L

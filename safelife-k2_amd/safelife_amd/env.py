@@ -90,6 +90,9 @@ class SafeLifeGame:
         venv = _single_venv(data, device, rng=rng, seed=seed)
         venv.reset()
         game = cls(venv, 0)
+        # deserialize leaves the level's own exit cells (the env reset coloured them)
+        _lib.check(_lib.lib().sl_env_exit_colors(ctypes.byref(game._slice()), 1, game._stream()),
+                   "sl_env_exit_colors")
         game.rescore()
         return game
 
@@ -125,6 +128,7 @@ class SafeLifeGame:
     def board(self, value):
         self._venv.board[self._idx].copy_(self._upload(value))
         self._set("spawn_flags", self._st("spawn_flags") | 1)   # may now hold a spawner
+        self._venv._may_spawn = True
         self.rescore()
 
     @property
@@ -135,6 +139,7 @@ class SafeLifeGame:
     def goals(self, value):
         self._venv.goals[self._idx].copy_(self._upload(value))
         self._set("spawn_flags", self._st("spawn_flags") | 2)
+        self._venv._may_spawn = True
         self._venv.planes_ok[self._idx].zero_()        # the goals mirror is stale
         self.rescore()
 
@@ -403,6 +408,7 @@ class SafeLifeGame:
             keep_start = (v.start_board[i].clone(), v.state["baseline"][i].clone())
         pool = LevelPool.from_levels([lvl])
         pdev = pool.to_device(v.device)
+        v._may_spawn = v._may_spawn or pool.has_spawners()
         cfg = v._fill_cfg()
         cfg.level_mode, cfg.augment_roll, cfg.env0, cfg.n_total_envs = 0, 0, 0, 1
         cfg.wrapper_min_performance = float("nan")

@@ -89,6 +89,10 @@ class LevelPool:
                     levels.append({k: d[k] for k in LEVEL_KEYS if k in d.files})
         return cls.from_levels(levels)
 
+    def has_spawners(self):
+        """Does any level's board or goals hold a spawning cell (CellTypes.spawning)?"""
+        return bool(((self.board | self.goals) & 0x80).any())
+
     def subset(self, idx):
         idx = np.asarray(idx)
         al = np.stack([self.agent_x[idx], self.agent_y[idx]], 1)

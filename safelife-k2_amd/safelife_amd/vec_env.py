@@ -104,6 +104,11 @@ class SafeLifeVecEnv:
         self._synced = (0, 0)        # (started, completed) already in global_counter
         self._recorder = None        # TrajectoryRecorder attached to this env
         self._alloc(obs_dtype)
+        # may any env's board or goals hold a spawning cell (bit 7)?  Spawners come only
+        # from levels (no rule or action creates one) unless powers can be toggled; when
+        # none can exist no uniform is ever drawn, and replay runs the Philox-form
+        # kernels (identical results, no count prologue / offsets scan)
+        self._may_spawn = self.pool.has_spawners()
         # the spaces of one env, as SafeLifeEnv declares them (safelife_env.py:97-109);
         # PPO reads them from envs[0] (training/ppo.py:219, safelife_ppo.py:196)
         self.action_space, self.observation_space = env_spaces(
@@ -193,6 +198,8 @@ class SafeLifeVecEnv:
             raise ValueError("empty level pool")
         self.pool = pool
         self._pool_dev = pool_dev if pool_dev is not None else pool.to_device(self.device)
+        # running envs keep their old-pool boards: the flag only grows here
+        self._may_spawn = self._may_spawn or pool.has_spawners()
         # running episodes' start boards are no longer levels of the pool: the
         # kernels read them from HBM until those envs are reset from the new pool
         self.st_t["start_roll"].fill_(-1)
@@ -234,7 +241,10 @@ class SafeLifeVecEnv:
         c.bonus_table = bt.data_ptr()
         c.bonus_len = bt.numel()
         c.bonus_period = self.movement_bonus_period
-        c.rng_mode = _lib.SL_RNG_STREAM if self.rng == "stream" else _lib.SL_RNG_PHILOX
+        if self.can_toggle_powers:      # a power toggle can make a spawner: sticky
+            self._may_spawn = True
+        replay = self.rng == "stream" and self._may_spawn
+        c.rng_mode = _lib.SL_RNG_STREAM if replay else _lib.SL_RNG_PHILOX
         c.seed = self.seed & 0xFFFFFFFFFFFFFFFF
         c.step = self._step_index & 0xFFFFFFFF
         c.env0 = self.env0
@@ -268,6 +278,8 @@ class SafeLifeVecEnv:
         if m is not None:
             running = running & (m.reshape(self.B) != 0)
         self._abandoned += int(running.sum().item())
+        if m is None:           # every env starts from the pool: only its levels count
+            self._may_spawn = self.pool.has_spawners()
         _lib.check(L.sl_env_reset(ctypes.byref(self._state), ctypes.byref(self._pool_dev["struct"]),
                                   _lib.ptr(m), ctypes.byref(cfg), _lib.stream_ptr(self.device)),
                    "sl_env_reset")
@@ -434,8 +446,9 @@ class SafeLifeVecEnv:
         return self.st_t
 
     def stream_error(self):
-        """True if rng='stream' ran past the end of the supplied stream."""
-        return bool(self.scratch[8 * self.B].item() & 1)
+        """True if rng='stream' ran past the end of the supplied stream (error word
+        bit 0), or a replay step's look-back gave up waiting (bit 1, never seen)."""
+        return bool(self.scratch[8 * self.B].item() & 3)
 
     def set_state(self, board, goals, start_board, **scalars):
         """Load explicit state (for tests / checkpoints).  Arrays are [B,...]."""
@@ -453,6 +466,7 @@ class SafeLifeVecEnv:
         mirrors are stale and the reset lists start empty."""
         self.st_t["start_roll"].fill_(-1)
         self.st_t["spawn_flags"].fill_(3)    # may hold spawners: replay counts them
+        self._may_spawn = True
         self.planes_ok.zero_()
         self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()
         self._last_step = None

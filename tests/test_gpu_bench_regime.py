@@ -229,3 +229,36 @@ def test_recorder_detached_mid_run(torch_dev, tmp_path, pool_name):
         for k in rec_env.st_t:
             assert torch.equal(rec_env.st_t[k], twin.st_t[k]), (t, k)
     assert n_reset >= B
+
+
+@pytest.mark.parametrize("config", ["c3", "c2"])
+def test_replay_without_spawners_is_philox_form(torch_dev, config):
+    """Levels with no spawning cell draw nothing (advance_board.c:101-113 needs a
+    spawner in the 3x3), so rng="stream" on such a pool runs the Philox-form kernels
+    (no count prologue, no offsets scan): same boards, rewards and flags as the
+    Philox env, the stream position never moves; a pool swap that brings spawners
+    switches the replay path back on."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool, _lib
+    fname, _ = CONFIGS[config]
+    pool = LevelPool.load(os.path.join(POOLS, fname))
+    assert not pool.has_spawners()
+    B = 512
+    kw = dict(KW, time_limit=40, level_order="random", augment_roll=True, seed=3)
+    rep = SafeLifeVecEnv(pool, B, dev, rng="stream", spawn_stream=np.random.rand(1000), **kw)
+    phx = SafeLifeVecEnv(pool, B, dev, rng="philox", **kw)
+    rep.reset()
+    phx.reset()
+    assert rep._fill_cfg().rng_mode == _lib.SL_RNG_PHILOX
+    g = torch.Generator(device=dev)
+    g.manual_seed(4)
+    for t in range(90):
+        a = torch.randint(0, 9, (B,), dtype=torch.int32, device=dev, generator=g)
+        _, r1, d1, i1 = rep.step(a)
+        _, r2, d2, i2 = phx.step(a)
+        assert torch.equal(r1, r2) and torch.equal(d1, d2), t
+        assert torch.equal(i1["reset"], i2["reset"]), t
+    assert torch.equal(rep.board, phx.board) and torch.equal(rep.goals, phx.goals)
+    assert int(rep.stream_pos.item()) == 0
+    rep.set_pool(_sprinkle(pool, 2, 0.02))
+    assert rep._fill_cfg().rng_mode == _lib.SL_RNG_STREAM
