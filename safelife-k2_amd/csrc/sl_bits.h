@@ -197,7 +197,6 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
 }
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // LDS slots compact_draws needs: one per 2x2 block a wave can hold (64 lanes x 16)
 constexpr int kDrawSlots = 1024;
 
@@ -347,79 +346,6 @@ __device__ __forceinline__ int stream_draws(const u32 elig[2], u32 sp[2], double
             }
     }
     return pre_a + pre_b;
-}
-
-// The same draws as stream_draws, with the uniforms read by the whole wave in stream
-// order.  The words' eligible cells (T of them, wave-uniform) take uniforms pos ..
-// pos + T - 1 in row-major order, so lane i of round r loads uniform pos + 64 r + i:
-// contiguous 512-byte loads, four rounds in flight together, and a round's compares
-// are one ballot, kept as a 64-bit mask in LDS (`bits`, >= 2 * ceil(T / 64) dwords).
-// Each eligible cell then reads its result at its rank (the per-row ballots of
-// stream_draws): one memory round trip per call instead of one per visited group
-// of four rows.  Returns T.
-template <bool SPLIT>
-__device__ __forceinline__ int stream_draws_lds(const u32 elig[2], u32 sp[2], double thr,
-                                                const StreamSrc &src, int64_t pos, int lane,
-                                                lds_u32 *bits) {
-    constexpr uint64_t even = 0x5555555555555555ull;
-    const bool odd = SPLIT && (lane & 1);
-    const uint64_t grp = SPLIT ? (odd ? ~even : even) : ~0ull;
-    const int own = __builtin_popcount(elig[0]) + __builtin_popcount(elig[1]);
-    const int total = wave_total(own);
-    sp[0] = 0u;
-    sp[1] = 0u;
-    if (thr <= 0.0 || thr >= 1.0) {              // the draws are consumed, never compared
-        if (thr >= 1.0) {
-            sp[0] = elig[0];
-            sp[1] = elig[1];
-        }
-        return total;
-    }
-    if (total == 0) return 0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // the last call's reads
-    __builtin_amdgcn_wave_barrier();
-    bool bad = false;
-#pragma unroll 1
-    for (int base = 0; base < total; base += 256) {
-        double u[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int k = base + 64 * r + lane;
-            const int64_t at = pos + k;
-            const bool in = k < total && at < src.n;
-            bad |= k < total && at >= src.n;
-            u[r] = in ? src.draws[at] : 1.0;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const uint64_t m = __ballot(u[r] < thr);
-            if (base + 64 * r < total && lane < 2)
-                bits[(base >> 5) + 2 * r + lane] = lane ? (u32)(m >> 32) : (u32)m;
-        }
-    }
-    if (bad) atomicOr((unsigned long long *)src.err, 1ull);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const int first = SPLIT ? wave_total(odd ? 0 : own) : 0;     // cells in rows 0..31
-    int pre_a = 0, pre_b = 0;
-#pragma unroll
-    for (int y = 0; y < 32; y++) {
-        const bool e0 = (elig[0] >> y) & 1u, e1 = (elig[1] >> y) & 1u;
-        const uint64_t m0 = __ballot(e0), m1 = __ballot(e1);
-        if ((m0 | m1) == 0ull) continue;
-        const int r0 = (odd ? first + pre_b : pre_a) + lanes_below(m0 & grp) +
-                       lanes_below(m1 & grp);
-        const int r1 = r0 + (e0 ? 1 : 0);
-        if (e0 && ((bits[r0 >> 5] >> (r0 & 31)) & 1u)) sp[0] |= 1u << y;
-        if (e1 && ((bits[r1 >> 5] >> (r1 & 31)) & 1u)) sp[1] |= 1u << y;
-        if (SPLIT) {
-            pre_a += __builtin_popcountll(m0 & even) + __builtin_popcountll(m1 & even);
-            pre_b += __builtin_popcountll(m0 & ~even) + __builtin_popcountll(m1 & ~even);
-        } else {
-            pre_a += __builtin_popcountll(m0) + __builtin_popcountll(m1);
-        }
-    }
-    return total;
 }
 
 // One CA step of the planes P (in place).  chg[w] = cells that changed.

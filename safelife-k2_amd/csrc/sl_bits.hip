@@ -55,7 +55,6 @@ struct Geo64 {
     StreamSrc src;     // SPAWN_STREAM: the supplied uniforms; pos = this tensor's first
     int64_t pos;
     int count;         // SPAWN_COUNT: this lane's eligible cells
-    lds_u32 *bits;     // SPAWN_STREAM: the compare bits of stream_draws_lds (128 dwords)
     template <class F>
     __device__ __forceinline__ V3 vert(const u32 *P, int w, F f) const {
         const u32 x = f(P, w);
@@ -75,7 +74,7 @@ struct Geo64 {
         if (MODE == SPAWN_PHILOX) {
             philox_spawn(*this, elig, sp, sc, tensor);
         } else if (MODE == SPAWN_STREAM) {
-            (void)stream_draws_lds<true>(elig, sp, sc.thr, src, pos, lane, bits);
+            (void)stream_draws<true>(elig, sp, sc.thr, src, pos, lane);
         } else {
             count += __builtin_popcount(elig[0]) + __builtin_popcount(elig[1]);
         }
@@ -86,6 +85,7 @@ struct Geo64 {
 // A wave's 8 KiB LDS buffer holds one 64x64 board, row-major, with the 16-byte
 // chunks of rows 32..63 rotated by 4 chunks so that the even (rows 0..31) and odd
 // (rows 32..63) lanes of a column-pair read fall in different banks.
+typedef __attribute__((address_space(3))) u32 lds_u32;
 
 __device__ __forceinline__ void dma_board(const uint16_t *__restrict__ src, lds_u32 *buf,
                                           int lane) {
@@ -445,7 +445,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
                                          const int32_t *__restrict__ actions, int ctp, int ctc,
                                          double *reward_out, uint8_t *done_out,
                                          uint8_t *flags_out, int32_t *ep_len_out,
-                                         int32_t *ep_rew_out, const Pre &pre, lds_u32 *dbits) {
+                                         int32_t *ep_rew_out, const Pre &pre) {
     const int64_t off = b * (int64_t)(N * N);
     const int lane_off = (lane & 1) * 1024 + (lane >> 1);     // dwords: row 32h, column pair j
     u32 *gb = reinterpret_cast<u32 *>(st.board + off) + lane_off;
@@ -493,7 +493,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
             transpose32(PG);
         }
         u32 cg[2];
-        rule_planes(PG, cg, Geo64<MODE>{lane, ssrc, pos_g, 0, dbits}, sc, 1u);
+        rule_planes(PG, cg, Geo64<MODE>{lane, ssrc, pos_g, 0}, sc, 1u);
         const u32 rg = wave_or(cg[0] | cg[1]);
         if (mg) {      // mirror: the words whose 32 cells changed (all of them if rebuilt)
             const bool all = !(pok & 2);
@@ -567,7 +567,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     transpose32(PB);
     const u32 erow = mux_edits(PB, ne, eidx, eval, lane);
     u32 cb[2];
-    rule_planes(PB, cb, Geo64<MODE>{lane, ssrc, pos_b, 0, dbits}, sc, 0u);
+    rule_planes(PB, cb, Geo64<MODE>{lane, ssrc, pos_b, 0}, sc, 0u);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- scores over the new board and goals
@@ -671,13 +671,11 @@ k_env_step_bits64(StepKArgs ka) {
     const int lane = threadIdx.x;
     __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
     lds_u32 *buf = (lds_u32 *)&stage[0];
-    // replay: the compare bits of a tensor's draws (stream_draws_lds, <= 4096 cells)
-    __shared__ __attribute__((aligned(8))) u32 dbits[MODE == SPAWN_STREAM ? 128 : 2];
     Pre pre;
     issue_pre(ka.st, ka.actions, b, lane, pre);
     dma_board(ka.st.board + b * (int64_t)(N * N), buf, lane);
     step_env<OBS, MODE>(ka.st, ka.a, ka.fx, b, lane, buf, ka.actions, ka.ctp, ka.ctc, ka.reward_out,
-                  ka.done_out, ka.flags_out, ka.ep_len_out, ka.ep_rew_out, pre, (lds_u32 *)dbits);
+                  ka.done_out, ka.flags_out, ka.ep_len_out, ka.ep_rew_out, pre);
 }
 
 // Replay-mode count of env b (SL_RNG_STREAM), one wave, after k_env_action (one lane
@@ -706,7 +704,7 @@ k_stream_prologue64(StepKArgs ka) {
     if (spf & 1) {
         load_pairs_nt<32>(reinterpret_cast<const u32 *>(st.board + off) + lane_off, P);
         transpose32(P);
-        Geo64<SPAWN_COUNT> gbd{lane, StreamSrc{nullptr, 0, nullptr}, 0, 0, nullptr};
+        Geo64<SPAWN_COUNT> gbd{lane, StreamSrc{nullptr, 0, nullptr}, 0, 0};
         rule_planes(P, ch, gbd, sc, 0u);
         nb = wave_total(gbd.count);
     }
@@ -722,7 +720,7 @@ k_stream_prologue64(StepKArgs ka) {
             load_pairs_nt<32>(reinterpret_cast<const u32 *>(st.goals + off) + lane_off, P);
             transpose32(P);
         }
-        Geo64<SPAWN_COUNT> ggl{lane, StreamSrc{nullptr, 0, nullptr}, 0, 0, nullptr};
+        Geo64<SPAWN_COUNT> ggl{lane, StreamSrc{nullptr, 0, nullptr}, 0, 0};
         rule_planes(P, ch, ggl, sc, 1u);
         ng = wave_total(ggl.count);
     }

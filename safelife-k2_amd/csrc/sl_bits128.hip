@@ -26,12 +26,8 @@
 //    their three colour planes are read, per band, for the scores;
 //  * the action (execute_action / move_agent, safelife_game.py:308-393) has run
 //    before this kernel: k_env_action (one lane per env, both RNG modes) leaves the
-//    state and cell edits in HBM and the reward in the scratch;
-//  * replay mode (the reference's stream order): each env counts its eligible cells
-//    first and finds its place in the stream by a decoupled look-back over the envs
-//    before it (stream_lookback), inside this kernel -- no count pass, no scan;
-//    the draws of a band are read by the whole wave in stream order and compared in
-//    one round trip (stream_draws_lds);
+//    state and cell edits in HBM and the reward in the scratch (in replay mode
+//    k_stream_prologue128 then counts the draws);
 //  * exits are rewritten by the epilogue after the band stores have completed.
 // Finished envs are queued and reset by a follow-up kernel (k_env_reset_list_wide,
 // one 1024-thread block per env).
@@ -49,7 +45,6 @@ namespace {
 // registers held across the rule (32.9 vs 37.1); prefetching the next band a band
 // ahead gave nothing (the start-board loads queue behind it, vmcnt is in order).
 constexpr int kMinWaves = 2;  // waves per SIMD the register budget is sized for
-constexpr int kMinWavesStream = 3;   // the replay form: 170 VGPRs unbounded (2 waves)
 
 constexpr int N = 128;       // rows = columns
 constexpr int RS = N / 2;    // dwords per row
@@ -77,8 +72,7 @@ struct GeoBand {
     int64_t pos;       // used = how many the band consumed
     int used;
     int count;         // SPAWN_COUNT: this lane's eligible cells
-    lds_u16 *slots;    // SPAWN_PHILOX: compact_draws' queue (kDrawSlots); SPAWN_STREAM:
-                       // stream_draws_lds' compare bits (512 B of it)
+    lds_u16 *slots;    // SPAWN_PHILOX: compact_draws' queue (kDrawSlots)
     template <class F>
     __device__ __forceinline__ V3 vert(const u32 *P, int w, F f) const {
         return vert_with(f(P, w), f(hv, w));
@@ -101,7 +95,7 @@ struct GeoBand {
         if (MODE == SPAWN_PHILOX) {
             philox_spawn_compact(*this, elig, sp, sc, tensor, slots);
         } else if (MODE == SPAWN_STREAM) {
-            used = stream_draws_lds<false>(elig, sp, sc.thr, src, pos, lane, (lds_u32 *)slots);
+            used = stream_draws<false>(elig, sp, sc.thr, src, pos, lane);
         } else {
             count += __builtin_popcount(elig[0]) + __builtin_popcount(elig[1]);
         }
@@ -149,86 +143,6 @@ __device__ __forceinline__ void pool_start_lds(const __attribute__((address_spac
     }
 }
 
-// Replay mode (SPAWN_STREAM): the eligible cells of one tensor, band by band -- the
-// uniforms it will draw this step (advance_board.c:101-113).  Default-policy loads:
-// the step reads the same rows again right after.
-__device__ __forceinline__ int count_eligible128(const u32 *g, int lane) {
-    SpawnCtx sc{0u, 0u, 0ull, 0.0};
-    const StreamSrc none{nullptr, 0, nullptr};
-    int n = 0;
-#pragma unroll 1
-    for (int t = 0; t < NB; t++) {
-        const int ru = (32 * t - 1) & (N - 1), rd = (32 * t + 32) & (N - 1);
-        const u32 up = g[ru * RS], dn = g[rd * RS];
-        u32 P[32];
-        load_pairs<RS>(g + 32 * t * RS, P);
-        transpose32(P);
-        GeoBand<SPAWN_COUNT> geo{lane, 32 * t, HaloView{up, dn}, none, 0, 0, 0, nullptr};
-        u32 ch[2];
-        rule_planes(P, ch, geo, sc, 0u);
-        n += geo.count;
-    }
-    return wave_total(n);
-}
-
-__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-// Replay mode: the stream position of env b's first uniform, by a decoupled look-back
-// over the envs before it in stream order (env after env: training/ppo.py:436-452,
-// random.c:47-52).  status[e] (scratch [6B, 7B), zeroed before the launch) is one
-// 8-byte word written by one agent-scope store: 0 = not yet, kAgg | env e's draw
-// count, kInc | the stream position after env e.  Env b publishes its count, then
-// reads 64 predecessors at a time (one per lane, agent-scope polls) back to the
-// nearest inclusive word, and publishes its own inclusive word.  Waves take env
-// indices from a ticket counter in start order, so every env a wave waits for is
-// held by a wave that has started: each publishes its count without waiting.
-constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kVal = kAgg - 1;
-
-__device__ __forceinline__ int64_t stream_lookback(uint64_t *status, int64_t b, int64_t total,
-                                                   const int64_t *stream_pos, int64_t *err,
-                                                   int lane) {
-    if (b == 0) {
-        const int64_t base = *stream_pos;
-        if (lane == 0)
-            __hip_atomic_store(&status[0], kInc | (uint64_t)(base + total), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        return base;
-    }
-    if (lane == 0)
-        __hip_atomic_store(&status[b], kAgg | (uint64_t)total, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    int64_t acc = 0, j0 = b - 1;
-    int spins = 0;
-    while (true) {
-        const int64_t j = j0 - lane;
-        const uint64_t w = j >= 0 ? __hip_atomic_load(&status[j], __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)
-                                  : 0ull;
-        const uint64_t inc = __ballot((w >> 62) == 2ull), rdy = __ballot((w >> 62) != 0ull);
-        const int k = inc ? __builtin_ctzll(inc) : 64;        // nearest inclusive word
-        const uint64_t need = k >= 63 ? ~0ull : ((2ull << k) - 1ull);
-        if ((rdy & need) != need) {        // a predecessor has not published yet
-            if (++spins > (1 << 20)) {     // never seen: flag it (scratch err bit 1)
-                if (lane == 0) atomicOr((unsigned long long *)err, 2ull);   // rather than hang
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        acc += wave_sum_i64(lane <= k ? (int64_t)(w & kVal) : 0);
-        if (k < 64) break;
-        j0 -= 64;
-    }
-    if (lane == 0)
-        __hip_atomic_store(&status[b], kInc | (uint64_t)(acc + total), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    return acc;
-}
-
 // all kernel arguments in one struct at kernarg offset 0: the epilogue re-reads its
 // pointers where it runs (kargs128()), so they are not held in SGPRs through the bands
 struct Step128KArgs {
@@ -250,24 +164,16 @@ __device__ __forceinline__ const Step128KArgs &kargs128() {
 
 // One env-step of env b, after the action: k_env_action has applied it -- state and cell edits in HBM, reward
 // in scratch act[b] -- so this kernel holds no action code, no edit lists and no
-// overlay.  MODE: SPAWN_PHILOX, or SPAWN_STREAM (the replay: the env's draws are
-// counted first and placed in the stream by stream_lookback; envs are taken in
-// ticket order).
+// overlay.  MODE: SPAWN_PHILOX, or SPAWN_STREAM (each tensor's first uniform from the
+// scratch offsets).
 template <int MODE>
-__global__ void __launch_bounds__(64, MODE == SPAWN_STREAM ? kMinWavesStream : kMinWaves)
+__global__ void __launch_bounds__(64, kMinWaves)
 k_env_step_bits128(Step128KArgs ka) {
     const sl_env_state &st = ka.st;
     const StepArgs &a = ka.a;
     const FastExtra &fx = ka.fx;
+    const int64_t b = blockIdx.x;
     const int lane = threadIdx.x;
-    int64_t b = blockIdx.x;
-    if (MODE == SPAWN_STREAM) {        // env index = the wave's place in start order
-        // (the ticket word, scratch [7B], is zeroed with the status words before the
-        // launch; exactly B waves take tickets 0 .. B-1)
-        int t = 0;
-        if (lane == 0) t = (int)atomicAdd((unsigned long long *)(fx.scratch + 7 * st.B), 1ull);
-        b = __builtin_amdgcn_readfirstlane(t);
-    }
     const int64_t off = b * (int64_t)(N * N);
     u32 *gb = reinterpret_cast<u32 *>(st.board + off) + lane;      // row r: gb[r * RS]
     u32 *gg = reinterpret_cast<u32 *>(st.goals + off) + lane;
@@ -277,7 +183,7 @@ k_env_step_bits128(Step128KArgs ka) {
     const u32 V = load_record(st, ka.actions, b, lane);
     __shared__ __attribute__((aligned(16))) u32 spool_[kPoolPlanes * 256];
     __attribute__((address_space(3))) u32 *spool = (__attribute__((address_space(3))) u32 *)spool_;
-    __shared__ __attribute__((aligned(16))) uint16_t slots_[kDrawSlots];
+    __shared__ uint16_t slots_[kDrawSlots];
     lds_u16 *slots = (lds_u16 *)slots_;
     const int pok = rec(V, R_POK) & 6;
     const Scratch w = scratch_of(fx.scratch, st.B);
@@ -291,19 +197,8 @@ k_env_step_bits128(Step128KArgs ka) {
     int64_t pos_b = 0, pos_g = 0;
     if (MODE == SPAWN_STREAM) {
         ssrc.err = w.err;
-        // a board or goals without spawners (spawn_flags, set at reset: no rule or
-        // action creates one) draws nothing; nor do goals at their fixed point
-        const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);     // toggling powers can make one
-        const int nb = (spf & 1) ? count_eligible128(gb, lane) : 0;
-        const int ng = ((pok & 6) == 6 || !(spf & 2)) ? 0 : count_eligible128(gg, lane);
-        pos_b = stream_lookback(reinterpret_cast<uint64_t *>(w.act + 2 * st.B), b, nb + ng,
-                                fx.stream_pos, w.err, lane);
-        pos_g = pos_b + nb;
-        if (lane == 0) {
-            w.offsets[2 * b] = pos_b;
-            w.offsets[2 * b + 1] = pos_g;
-            if (b == st.B - 1) *fx.stream_pos = pos_g + ng;
-        }
+        pos_b = w.offsets[2 * b];
+        pos_g = w.offsets[2 * b + 1];
     }
     // Bands are processed in order 0..3, so the pre-step halo rows of band t are band
     // t - 1's last row (kept from its load: it is written back before band t runs),
@@ -440,6 +335,52 @@ k_env_step_bits128(Step128KArgs ka) {
     }
 }
 
+// Replay-mode count of env b (SL_RNG_STREAM), one wave, after k_env_action (one lane
+// per env) has applied the actions -- state and cell edits in HBM, rewards in scratch
+// act[] -- so the board read here is the acted-on one: the eligible cells of the board
+// and of the goals, band by band (scratch counts[2b], [2b+1]; sl_exclusive_scan_i64
+// turns them into each tensor's first uniform).  The work of k_env_count (sl_env.hip)
+// on the bit-sliced rule.
+__global__ void __launch_bounds__(64)
+k_stream_prologue128(Step128KArgs ka) {
+    const sl_env_state &st = ka.st;
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t off = b * (int64_t)(N * N);
+    const u32 *gb = reinterpret_cast<const u32 *>(st.board + off) + lane;
+    const u32 *gg = reinterpret_cast<const u32 *>(st.goals + off) + lane;
+    const u32 V = load_record(st, ka.actions, b, lane);
+    const Scratch w = scratch_of(ka.fx.scratch, st.B);
+    SpawnCtx sc{0u, 0u, 0ull, 0.0};
+    const StreamSrc none{nullptr, 0, nullptr};
+    // the eligible cells of one tensor, band by band
+    auto count = [&](const u32 *g) {
+        int n = 0;
+#pragma unroll 1
+        for (int t = 0; t < NB; t++) {
+            const int ru = (32 * t - 1) & (N - 1), rd = (32 * t + 32) & (N - 1);
+            const u32 up = g[ru * RS], dn = g[rd * RS];
+            u32 P[32];
+            load_pairs_nt<RS>(g + 32 * t * RS, P);
+            transpose32(P);
+            GeoBand<SPAWN_COUNT> geo{lane, 32 * t, HaloView{up, dn}, none, 0, 0, 0, nullptr};
+            u32 ch[2];
+            rule_planes(P, ch, geo, sc, 0u);
+            n += geo.count;
+        }
+        return wave_total(n);
+    };
+    // a board or goals without spawners (spawn_flags, set at reset: no rule or action
+    // creates one) draws nothing; nor do goals at their fixed point (planes_ok bit 2)
+    const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);     // toggling powers can make one
+    const int nb = (spf & 1) ? count(gb) : 0;
+    const int ng = ((rec(V, R_POK) & 6) == 6 || !(spf & 2)) ? 0 : count(gg);
+    if (lane == 0) {
+        w.counts[2 * b] = nb;
+        w.counts[2 * b + 1] = ng;
+    }
+}
+
 }  // namespace
 
 namespace sl {
@@ -455,14 +396,12 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
     const Step128KArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
     const dim3 grid((unsigned)st.B);
     if (fx.stream) {
-        const Scratch w = scratch_of(fx.scratch, st.B);
-        const int rca = launch_env_action(st, actions, ctp, ctc, w.act, s);
+        const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
         if (rca) return rca;
-        // the look-back status words start at "not yet" (stream_lookback) and the
-        // ticket word after them at 0
-        if (hipMemsetAsync(w.act + 2 * st.B, 0, (size_t)(st.B + 1) * sizeof(int64_t), s) !=
-            hipSuccess)
-            return SL_EHIP;
+        hipLaunchKernelGGL(k_stream_prologue128, grid, dim3(64), 0, s, ka);
+        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        const int rc = stream_offsets(st, fx, s);
+        if (rc) return rc;
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
         hipLaunchKernelGGL(k_env_step_bits128<SPAWN_STREAM>, grid, dim3(64), 0, s, ka);
     } else {

@@ -90,6 +90,7 @@ __device__ __forceinline__ GeoSmall<MODE> small_geo(int lane, int H, int W) {
     return g;
 }
 
+typedef __attribute__((address_space(3))) u32 lds_u32;
 typedef __attribute__((address_space(3))) const uint16_t lds_cu16;
 
 // unedited cells for the action, from the staged board: row y is 32 dwords, and the

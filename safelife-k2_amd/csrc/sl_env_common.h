@@ -11,10 +11,8 @@ namespace sl {
 //             envs to reset after the step (64x64 and 128x128 kernels)
 //   [2B, 4B)  per-(env, tensor) stream offsets   (replay mode)
 //   [4B, 8B)  per env: action reward, d_points, d_score, d_side of the action's
-//             cell edits (the generic path; k_env_action<false> -- the bit-sliced
-//             replay and 128x128 pre-pass -- writes the reward only); the 128x128
-//             replay step keeps its look-back status words in [6B, 7B) and its
-//             ticket counter in [7B] (both zeroed before each launch)
+//             cell edits (the generic path; the bit-sliced replay prologues write
+//             the reward only)
 //   [8B]      error flags (bit0: draw stream exhausted)
 //   [8B+2], [8B+3]  reset-list lengths for even / odd steps (each step's reset
 //             kernel zeroes the other one)

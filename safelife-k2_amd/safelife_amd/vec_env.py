@@ -446,9 +446,8 @@ class SafeLifeVecEnv:
         return self.st_t
 
     def stream_error(self):
-        """True if rng='stream' ran past the end of the supplied stream (error word
-        bit 0), or a replay step's look-back gave up waiting (bit 1, never seen)."""
-        return bool(self.scratch[8 * self.B].item() & 3)
+        """True if rng='stream' ran past the end of the supplied stream."""
+        return bool(self.scratch[8 * self.B].item() & 1)
 
     def set_state(self, board, goals, start_board, **scalars):
         """Load explicit state (for tests / checkpoints).  Arrays are [B,...]."""
