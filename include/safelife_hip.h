@@ -316,6 +316,21 @@ typedef struct sl_env_cfg {
     int32_t obs_channels[16];
     const sl_capture *capture;      /* host pointer or NULL: trajectory capture
                                        (needs auto_reset and info_flags)      */
+    int32_t stream_phase;           /* SL_RNG_STREAM with the batch split over
+                                       shards (SURVEY §8(e) collective 3: the
+                                       reference's one stream runs env after env
+                                       over ALL shards, training/ppo.py:436-452):
+                                       0 = the whole step, this batch alone;
+                                       1 = count phase: the actions, then each
+                                       env's eligible cells; *stream_pos = this
+                                       batch's draw total (no draw, no advance);
+                                       2 = draw phase (after a phase-1 call on the
+                                       same state): this batch's draws start at
+                                       *stream_base -- the global position plus
+                                       the totals of the shards before it --, the
+                                       step completes, *stream_pos = *stream_base
+                                       + the batch's total                     */
+    const int64_t *stream_base;     /* dev [1]: phase 2's first uniform        */
 } sl_env_cfg;
 
 /*

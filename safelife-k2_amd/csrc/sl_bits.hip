@@ -768,12 +768,14 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
     if (fx.obs_out && (fx.obs_vh < 1 || fx.obs_vw < 1 || fx.obs_vh * fx.obs_vw > 4096))
         return SL_EINVAL;
     if (fx.stream) {
-        const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
-        if (rca) return rca;
-        hipLaunchKernelGGL(k_stream_prologue64, dim3(grid), dim3(64), 0, s, ka);
-        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        if (stream_counts(fx)) {
+            const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
+            if (rca) return rca;
+            hipLaunchKernelGGL(k_stream_prologue64, dim3(grid), dim3(64), 0, s, ka);
+            if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        }
         const int rc = stream_offsets(st, fx, s);
-        if (rc) return rc;
+        if (rc || !stream_steps(fx)) return rc;
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
         if (fx.obs_out)
             hipLaunchKernelGGL((k_env_step_bits64<true, SPAWN_STREAM>), dim3(grid), dim3(64), 0, s, ka);

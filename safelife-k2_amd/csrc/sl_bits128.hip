@@ -396,12 +396,14 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
     const Step128KArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
     const dim3 grid((unsigned)st.B);
     if (fx.stream) {
-        const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
-        if (rca) return rca;
-        hipLaunchKernelGGL(k_stream_prologue128, grid, dim3(64), 0, s, ka);
-        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        if (stream_counts(fx)) {
+            const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
+            if (rca) return rca;
+            hipLaunchKernelGGL(k_stream_prologue128, grid, dim3(64), 0, s, ka);
+            if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        }
         const int rc = stream_offsets(st, fx, s);
-        if (rc) return rc;
+        if (rc || !stream_steps(fx)) return rc;
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
         hipLaunchKernelGGL(k_env_step_bits128<SPAWN_STREAM>, grid, dim3(64), 0, s, ka);
     } else {

@@ -971,13 +971,15 @@ int launch_step_small(const sl_env_state &st, const StepArgs &a, const FastExtra
     const dim3 grid4((unsigned)((st.B + 3) / 4));
     const size_t lds4 = (size_t)3 * seg_stride(st.H, st.W) * sizeof(uint16_t);
     if (fx.stream) {
-        const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
-        if (rca) return rca;
-        hipLaunchKernelGGL(k_stream_prologue_small, grid, dim3(64), (size_t)2 * st.H * 32 * sizeof(uint32_t),
-                           s, ka);
-        if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        if (stream_counts(fx)) {
+            const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
+            if (rca) return rca;
+            hipLaunchKernelGGL(k_stream_prologue_small, grid, dim3(64),
+                               (size_t)2 * st.H * 32 * sizeof(uint32_t), s, ka);
+            if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        }
         const int rc = stream_offsets(st, fx, s);
-        if (rc) return rc;
+        if (rc || !stream_steps(fx)) return rc;
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
         if (seg && dppn)
             hipLaunchKernelGGL((k_env_step_seg4<SPAWN_STREAM, true>), grid4, dim3(64), lds4, s, ka);

@@ -1031,8 +1031,11 @@ extern "C" int sl_level_pool_prepare(sl_level_pool *pool, void *stream) {
 
 int sl::stream_offsets(const sl_env_state &st, const FastExtra &fx, hipStream_t s) {
     const Scratch sc = scratch_of(fx.scratch, st.B);
-    return sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * st.B, fx.stream_pos, fx.stream_pos,
-                                 (void *)s);
+    // phase 0: from the stream position; 1: from 0 (only the total matters, it lands
+    // in *stream_pos); 2: from the shard's base the caller placed in *stream_base
+    const int64_t *base = fx.stream_phase == 1 ? nullptr
+                          : fx.stream_phase == 2 ? fx.stream_base : fx.stream_pos;
+    return sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * st.B, base, fx.stream_pos, (void *)s);
 }
 
 extern "C" int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const uint8_t *mask,
@@ -1077,6 +1080,9 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     if (cfg->rng_mode != SL_RNG_STREAM && cfg->rng_mode != SL_RNG_PHILOX) return SL_EINVAL;
     const bool replay = cfg->rng_mode == SL_RNG_STREAM;
     if (replay && (!cfg->stream_pos || (!cfg->draws && cfg->n_draws > 0))) return SL_EINVAL;
+    if (cfg->stream_phase < 0 || cfg->stream_phase > 2 || (cfg->stream_phase && !replay) ||
+        (cfg->stream_phase == 2 && !cfg->stream_base))
+        return SL_EINVAL;
     const bool bits_ok = cfg->kernel != SL_KERNEL_GENERIC;
     const bool fast = bits_ok && st->H == 64 && st->W == 64;
     const bool fast128 = bits_ok && bits128_shape(*st);
@@ -1098,6 +1104,8 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     fx.capture = cap;
     fx.stream = replay ? 1 : 0;
     fx.stream_pos = cfg->stream_pos;
+    fx.stream_phase = cfg->stream_phase;
+    fx.stream_base = cfg->stream_base;
     fx.ev_begin = cfg->ev_begin;
     // the small-board kernel resets finished envs inside the step; with a capture the
     // resets run in the follow-up scan so the pre-reset frame can be copied first.
@@ -1122,31 +1130,35 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         int rc = launch_step_bits128(*st, a, fx, actions, cfg->can_toggle_powers,
                                      cfg->can_toggle_colors, reward, done, info_flags, ep_len,
                                      ep_reward, s);
-        if (rc) return rc;
+        if (rc || cfg->stream_phase == 1) return rc;
         reset_done = fx.fuse_reset && fx.pool.K > 0;
     } else if (small) {
         int rc = launch_step_small(*st, a, fx, actions, cfg->can_toggle_powers,
                                    cfg->can_toggle_colors, reward, done, info_flags, ep_len,
                                    ep_reward, s);
-        if (rc) return rc;
+        if (rc || cfg->stream_phase == 1) return rc;
         reset_done = fx.fuse_reset && fx.pool.K > 0 && fx.pool.H == st->H && fx.pool.W == st->W;
     } else if (fast) {
         int rc = launch_step_bits(*st, a, fx, actions, cfg->can_toggle_powers,
                                   cfg->can_toggle_colors, reward, done, info_flags, ep_len,
                                   ep_reward, s);
-        if (rc) return rc;
+        if (rc || cfg->stream_phase == 1) return rc;
         reset_done = fx.fuse_reset && fx.pool.K > 0;
     } else {
-        hipLaunchKernelGGL(k_env_action<true>, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s,
-                           *st, actions, cfg->can_toggle_powers, cfg->can_toggle_colors, sc.act);
-        if (hipGetLastError() != hipSuccess) return SL_EHIP;
-        if (replay) {
-            if (!set_lds((const void *)k_env_count, lds)) return SL_ETOOBIG;
-            hipLaunchKernelGGL(k_env_count, dim3((unsigned)B), dim3(NT), lds, s, *st, sc.counts);
+        if (!replay || stream_counts(fx)) {
+            hipLaunchKernelGGL(k_env_action<true>, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
+                               s, *st, actions, cfg->can_toggle_powers, cfg->can_toggle_colors,
+                               sc.act);
             if (hipGetLastError() != hipSuccess) return SL_EHIP;
-            int rc = sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * B, cfg->stream_pos,
-                                           cfg->stream_pos, stream);
-            if (rc) return rc;
+        }
+        if (replay) {
+            if (stream_counts(fx)) {
+                if (!set_lds((const void *)k_env_count, lds)) return SL_ETOOBIG;
+                hipLaunchKernelGGL(k_env_count, dim3((unsigned)B), dim3(NT), lds, s, *st, sc.counts);
+                if (hipGetLastError() != hipSuccess) return SL_EHIP;
+            }
+            int rc = stream_offsets(*st, fx, s);
+            if (rc || cfg->stream_phase == 1) return rc;
             if (!set_lds((const void *)k_env_step_generic<SL_RNG_STREAM>, lds)) return SL_ETOOBIG;
             hipLaunchKernelGGL(k_env_step_generic<SL_RNG_STREAM>, dim3((unsigned)B), dim3(NT), lds,
                                s, *st, a, sc.act, sc.offsets, sc.err, reward, done, info_flags,

@@ -304,7 +304,14 @@ struct FastExtra {
                             // offsets scan, then the step kernel's SPAWN_STREAM form
     int64_t *stream_pos;    // replay mode: the stream position (in / out, device)
     void *ev_begin;         // hipEvent_t recorded right before the step kernel, or NULL
+    int32_t stream_phase;   // replay split over shards (sl_env_cfg.stream_phase): 0
+                            // whole step, 1 action + counts + total, 2 offsets from
+    const int64_t *stream_base;   // *stream_base + the step
 };
+// replay-mode phases of a bit-sliced launcher: whether it runs the action + count
+// prologue, and whether it continues past the offsets scan to the step kernel
+__host__ inline bool stream_counts(const FastExtra &fx) { return fx.stream_phase != 2; }
+__host__ inline bool stream_steps(const FastExtra &fx) { return fx.stream_phase != 1; }
 // replay mode: exclusive scan of the prologue's per-(env, tensor) eligible counts into
 // each tensor's first uniform, advancing *fx.stream_pos (sl_env.hip)
 int stream_offsets(const sl_env_state &st, const FastExtra &fx, hipStream_t s);

@@ -63,7 +63,7 @@ class EnvCfg(ctypes.Structure):
                 ("ev_begin", vp), ("ev_end", vp), ("kernel", i32),
                 ("obs_out", vp), ("obs_mode", i32), ("obs_vh", i32), ("obs_vw", i32),
                 ("obs_remove_white", i32), ("obs_nch", i32), ("obs_channels", i32 * 16),
-                ("capture", vp)]
+                ("capture", vp), ("stream_phase", i32), ("stream_base", vp)]
 
 
 class Capture(ctypes.Structure):

@@ -12,6 +12,14 @@ collective.  Collectives run at logging cadence only:
 * :func:`gather_episodes` -- all_gather of finished-episode records
   (return, length, ...), padded to the largest shard's count.
 
+Parity mode is the exception (SURVEY.md §8(e) collective 3): the reference draws
+every spawn uniform from ONE stream, env after env over the whole batch
+(training/ppo.py:436-452, random.c:47-52), so a shard's draws start where the
+shards before it end.  :class:`StreamExchange` is that per-step exchange: one int64
+per rank (the shard's draw total of the step) all-gathered, each rank's base = the
+global position plus the totals of the ranks before it (SafeLifeVecEnv's
+``stream_exchange``; sl_env_cfg.stream_phase).
+
 Works with any ``torch.distributed`` backend: ``nccl`` (RCCL over xGMI) on the
 GPU box, ``gloo`` in the CPU tests.
 """
@@ -78,3 +86,42 @@ def gather_episodes(records, device=None):
     outs = [torch.zeros_like(pad) for _ in range(world)]
     dist.all_gather(outs, pad)
     return torch.cat([o[:c] for o, c in zip(outs, counts)], 0)
+
+
+class StreamExchange:
+    """Places each shard's reference-order draws in the one global stream.
+
+    ``pos`` (a device int64 [1]) is the global stream position, identical on every
+    rank.  Called with the shard's draw total of the step (device int64 [1], what
+    the count phase leaves in the env's stream_pos), it all-gathers the totals of
+    every rank (one int64 each: RCCL over xGMI on the GPU box, gloo on the CPU),
+    returns this rank's base -- pos + the totals of the lower ranks -- and advances
+    pos past all of them.  Stream-ordered, no host synchronisation.  Without an
+    initialised process group it is the single-rank exchange (base = pos).
+    """
+
+    def __init__(self, device=None, pos=0, group=None):
+        import torch
+        self.group = group
+        self.pos = torch.tensor([int(pos)], dtype=torch.int64, device=device)
+
+    def _world(self):
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(self.group), dist.get_rank(self.group)
+        return 1, 0
+
+    def __call__(self, local_total):
+        import torch
+        import torch.distributed as dist
+        world, rank = self._world()
+        local_total = local_total.reshape(1).to(torch.int64)
+        if world == 1:
+            totals = local_total
+        else:
+            parts = [torch.zeros_like(local_total) for _ in range(world)]
+            dist.all_gather(parts, local_total, group=self.group)
+            totals = torch.cat(parts)
+        base = self.pos + totals[:rank].sum()
+        self.pos += totals.sum()
+        return base

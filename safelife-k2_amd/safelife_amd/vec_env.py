@@ -64,7 +64,7 @@ class SafeLifeVecEnv:
                  auto_reset=True, rng="philox", seed=0, spawn_stream=None,
                  level_order="sequential", augment_roll=False, env0=0, n_total_envs=None,
                  can_toggle_powers=False, can_toggle_colors=False, obs_dtype="uint16",
-                 compute_obs=True, global_counter=None, kernel="auto"):
+                 compute_obs=True, global_counter=None, kernel="auto", stream_exchange=None):
         import torch
         self.torch = torch
         self.device = _lib.require_device(device)
@@ -95,6 +95,9 @@ class SafeLifeVecEnv:
         self.kernel = {"auto": _lib.SL_KERNEL_AUTO, "generic": _lib.SL_KERNEL_GENERIC,
                        "fast": _lib.SL_KERNEL_FAST}[kernel]
         self.global_counter = global_counter if global_counter is not None else GlobalCounter()
+        # rng="stream" over shards: dist.StreamExchange (or any callable of the same
+        # contract) places this shard's draws in the global stream every step
+        self.stream_exchange = stream_exchange
         self._step_index = 0
         # step index and auto_reset flag of the last launched step: the 64x64 and
         # 128x128 kernels queue finished envs in per-parity lists (sl_env_cfg.scratch)
@@ -243,7 +246,9 @@ class SafeLifeVecEnv:
         c.bonus_period = self.movement_bonus_period
         if self.can_toggle_powers:      # a power toggle can make a spawner: sticky
             self._may_spawn = True
-        replay = self.rng == "stream" and self._may_spawn
+        # (shards exchange totals every step whether or not they can draw, so every
+        # rank makes the same collective calls)
+        replay = self.rng == "stream" and (self._may_spawn or self.stream_exchange is not None)
         c.rng_mode = _lib.SL_RNG_STREAM if replay else _lib.SL_RNG_PHILOX
         c.seed = self.seed & 0xFFFFFFFFFFFFFFFF
         c.step = self._step_index & 0xFFFFFFFF
@@ -255,6 +260,8 @@ class SafeLifeVecEnv:
             c.draws = None
             c.n_draws = 0
         c.stream_pos = self.stream_pos.data_ptr()
+        c.stream_phase = 0
+        c.stream_base = None
         c.scratch = self.scratch.data_ptr()
         c.level_mode = 1 if self.level_order == "random" else 0
         c.n_total_envs = self.n_total_envs
@@ -360,15 +367,23 @@ class SafeLifeVecEnv:
         if self.compute_obs or obs_out is not None:
             obs = self.obs if obs_out is None else self._obs_target(obs_out)
         self._fill_obs_cfg(cfg, obs)
-        _lib.check(L.sl_env_step(ctypes.byref(self._state), ctypes.byref(self._pool_dev["struct"]),
-                                 a.data_ptr(), ctypes.byref(cfg),
-                                 self._out(reward_out, self.reward).data_ptr(),
-                                 self._out(done_out, self.done).data_ptr(),
-                                 self._out(flags_out, self.flags).data_ptr(),
-                                 self._out(ep_len_out, self.ep_len).data_ptr(),
-                                 self._out(ep_rew_out, self.ep_rew).data_ptr(),
-                                 _lib.stream_ptr(self.device)),
-                   "sl_env_step")
+        outs = [self._out(reward_out, self.reward), self._out(done_out, self.done),
+                self._out(flags_out, self.flags), self._out(ep_len_out, self.ep_len),
+                self._out(ep_rew_out, self.ep_rew)]
+
+        def launch():
+            _lib.check(L.sl_env_step(ctypes.byref(self._state),
+                                     ctypes.byref(self._pool_dev["struct"]), a.data_ptr(),
+                                     ctypes.byref(cfg), *[o.data_ptr() for o in outs],
+                                     _lib.stream_ptr(self.device)), "sl_env_step")
+        if cfg.rng_mode == _lib.SL_RNG_STREAM and self.stream_exchange is not None:
+            # parity mode over shards: counts -> totals exchanged -> this shard's base
+            cfg.stream_phase = 1
+            launch()
+            self._stream_base = self.stream_exchange(self.stream_pos)
+            cfg.stream_phase = 2
+            cfg.stream_base = self._stream_base.data_ptr()
+        launch()
         self._step_index += 1
         self.global_counter.num_steps += self.B
 

@@ -262,3 +262,44 @@ def test_replay_without_spawners_is_philox_form(torch_dev, config):
     assert int(rep.stream_pos.item()) == 0
     rep.set_pool(_sprinkle(pool, 2, 0.02))
     assert rep._fill_cfg().rng_mode == _lib.SL_RNG_STREAM
+
+
+@pytest.mark.parametrize("config,frac,B", [("c5", 0.0, 64), ("c3", 0.01, 256),
+                                           ("c2", 0.02, 256)])
+def test_replay_shards_chained_through_stream_base(torch_dev, config, frac, B):
+    """SURVEY §8(e) collective 3 on one GPU: two shard envs (env0 = 0 and B/2) whose
+    replay draws are placed by one StreamExchange -- each step's count phase gives a
+    shard's draw total, the exchange its base (the global position plus the totals of
+    the shards before it), the draw phase steps from there -- reproduce one B-env
+    replay run bit for bit: rewards, done flags, boards, goals and the stream
+    position (the reference's single stream, env after env: training/ppo.py:436-452)."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    from safelife_amd import dist as sdist
+    fname, _ = CONFIGS[config]
+    pool = LevelPool.load(os.path.join(POOLS, fname))
+    if frac:
+        pool = _sprinkle(pool, 13, frac)
+    g = torch.Generator(device=dev)
+    g.manual_seed(17)
+    stream = torch.rand(8_000_000, dtype=torch.float64, device=dev, generator=g)
+    kw = dict(KW, time_limit=25, level_order="random", augment_roll=True, seed=9,
+              spawn_stream=stream, rng="stream", kernel="fast")
+    whole = SafeLifeVecEnv(pool, B, dev, **kw)
+    ex = sdist.StreamExchange(device=dev)
+    shards = [SafeLifeVecEnv(pool, B // 2, dev, env0=r * (B // 2), n_total_envs=B,
+                             stream_exchange=ex, **kw) for r in range(2)]
+    assert torch.equal(whole.reset(), torch.cat([s.reset() for s in shards]))
+    for t in range(60):
+        a = torch.randint(0, 9, (B,), dtype=torch.int32, device=dev, generator=g)
+        _, r, d, info = whole.step(a)
+        outs = [s.step(a[i * (B // 2):(i + 1) * (B // 2)]) for i, s in enumerate(shards)]
+        assert torch.equal(r, torch.cat([o[1] for o in outs])), t
+        assert torch.equal(d, torch.cat([o[2] for o in outs])), t
+        assert int(whole.stream_pos.item()) == int(ex.pos.item()), t
+        assert int(shards[1].stream_pos.item()) == int(ex.pos.item()), t
+        if t % 10 == 9:
+            assert torch.equal(whole.board, torch.cat([s.board for s in shards])), t
+            assert torch.equal(whole.goals, torch.cat([s.goals for s in shards])), t
+    assert int(ex.pos.item()) > 0
+    assert not whole.stream_error() and not any(s.stream_error() for s in shards)
