@@ -223,9 +223,18 @@ typedef struct sl_env_state {
                                  bit 1 is set.                                 */
     int32_t *planes_ok;       /* [B] bit1: goals mirror valid; bit2: goals at
                                  a fixed point (no spawner, unchanged by the
-                                 last step: the rule is skipped).  Anything
+                                 last step: the rule is skipped); bit3: board
+                                 count mirror (elig_planes) valid.  Anything
                                  that writes the goals other than the 64x64
                                  kernel and its reset clears it.               */
+    uint32_t *elig_planes;    /* replay mode, 128x128: the board's planes 0, 4,
+                                 6, 7 (alive, frozen, inhibiting, spawning) --
+                                 all an eligible-cell count reads -- written by
+                                 the replay step, patched by the action pre-pass,
+                                 read by the next step's count (8 KiB per env
+                                 instead of the 32 KiB board):
+                                 [B][band t][s][word w][lane], s = 0..3 for
+                                 planes 0, 4, 6, 7; or NULL                     */
 } sl_env_state;
 
 /* A device-resident level pool (the level_iterator's levels). */

@@ -506,13 +506,20 @@ __device__ __forceinline__ u32 colour_in(u32 c0, u32 c1, u32 c2, int s) {
 //   score    = sum sign(point_table)[g, c] * m,  m = alive & !(frozen & !movable)  (:601-631)
 //   possible = sum [g not in {black, white}]
 //   side     = #cells that are a side effect                      (env_wrappers.py:326-342)
+// GC_IN_B: the goal colour planes are B's planes 12-14 (the fused-view kernel puts
+// them there when the board's own bits 12-14 are all clear, so those bits count as 0
+// in the side-effect compare; white goals may be cleared: rows black and white of the
+// point table are equal, and neither counts as possible); gc is then not read.
+template <bool GC_IN_B = false>
 __device__ __forceinline__ void score_planes(const u32 B[32], const u32 gc[3][2], const u32 S[32],
                                              int *pts, int *scr, int *pos, int *side) {
     int p = 0, q = 0, r = 0, e = 0;
 #pragma unroll
     for (int w = 0; w < 2; w++) {
         const u32 c0 = PL(B, 9, w), c1 = PL(B, 10, w), c2 = PL(B, 11, w);
-        const u32 g0 = gc[0][w], g1 = gc[1][w], g2 = gc[2][w];
+        const u32 g0 = GC_IN_B ? PL(B, 12, w) : gc[0][w];
+        const u32 g1 = GC_IN_B ? PL(B, 13, w) : gc[1][w];
+        const u32 g2 = GC_IN_B ? PL(B, 14, w) : gc[2][w];
         u32 m5 = 0, m3 = 0, m1 = 0, mm3 = 0;
 #pragma unroll
         for (int g = 0; g < 8; g++) {
@@ -532,7 +539,8 @@ __device__ __forceinline__ void score_planes(const u32 B[32], const u32 gc[3][2]
         u32 d = PL(B, 0, w) ^ PL(S, 0, w);
         d |= PL(B, 2, w) ^ PL(S, 2, w);
 #pragma unroll
-        for (int k = 7; k < 16; k++) d |= PL(B, k, w) ^ PL(S, k, w);
+        for (int k = 7; k < 16; k++)
+            d |= ((GC_IN_B && k >= 12 && k <= 14) ? 0u : PL(B, k, w)) ^ PL(S, k, w);
         const u32 start_red_gone = PL(S, 0, w) & PL(S, 9, w) & ~(PL(B, 0, w) & PL(B, 9, w));
         const u32 blue_goal_alive = g2 & ~g1 & ~g0 & PL(B, 0, w) & ~PL(B, 9, w);
         e += __builtin_popcount(d & ~PL(S, 8, w) & ~start_red_gone & ~blue_goal_alive);

@@ -569,6 +569,21 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     u32 cb[2];
     rule_planes(PB, cb, Geo64<MODE>{lane, ssrc, pos_b, 0}, sc, 0u);
     __builtin_amdgcn_sched_barrier(0);
+    // fused views: board bits 12-14 are unused by every cell type, so (wave-uniform
+    // check) the goal colours go into planes 12-14 now -- the scores read them there
+    // and the goal planes die before the scoring -- and ONE transpose later yields
+    // both the board rows and the view rows
+    const bool hi = OBS && __ballot((PL(PB, 12, 0) | PL(PB, 13, 0) | PL(PB, 14, 0) |
+                                     PL(PB, 12, 1) | PL(PB, 13, 1) | PL(PB, 14, 1)) != 0u) != 0ull;
+    if (OBS && !hi) {
+        const int obs_rw = kernarg().fx.obs_rw;
+#pragma unroll
+        for (int w = 0; w < 2; w++) {
+            const u32 white = obs_rw ? (gcol[0][w] & gcol[1][w] & gcol[2][w]) : 0u;
+#pragma unroll
+            for (int k = 0; k < 3; k++) PL(PB, 12 + k, w) = gcol[k][w] & ~white;
+        }
+    }
 
     // ---- scores over the new board and goals
     u32 PS[32];
@@ -580,7 +595,8 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         transpose32(PS);
     }
     int pts, scr, pos, side;
-    score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
+    if (OBS && !hi) score_planes<true>(PB, gcol, PS, &pts, &scr, &pos, &side);
+    else score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
     // totals (packed two per word: per-lane ranges [-192, 320] and [-64, 64]);
     // reduced before the board store so the scoring is not sunk past it
     const int s1 = wave_total((pts + 192) | ((scr + 64) << 16));
@@ -600,52 +616,22 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
 #pragma unroll
         for (int w = 0; w < 2; w++)
             PL(PB, 9, w) = can ? (PL(PB, 9, w) | PL(PB, 8, w)) : (PL(PB, 9, w) & ~PL(PB, 8, w));
-        const bool hi = OBS && __ballot((PL(PB, 12, 0) | PL(PB, 13, 0) | PL(PB, 14, 0) |
-                                         PL(PB, 12, 1) | PL(PB, 13, 1) | PL(PB, 14, 1)) != 0u) != 0ull;
-        const int obs_rw = OBS ? kernarg().fx.obs_rw : 0;
-        const u32(&gv)[3][2] = gcol;
+        transpose32(PB);
         if (OBS && !hi) {
-            // planes 12-14 := goal colours; the store masks them out again
-#pragma unroll
-            for (int w = 0; w < 2; w++) {
-                const u32 white = obs_rw ? (gv[0][w] & gv[1][w] & gv[2][w]) : 0u;
-#pragma unroll
-                for (int k = 0; k < 3; k++) PL(PB, 12 + k, w) = gv[k][w] & ~white;
-            }
-            transpose32(PB);
+            // planes 12-14 hold the goal colours: the store masks them out again
             if (rb) {
 #pragma unroll
                 for (int y = 0; y < 32; y++)
                     if ((rb >> y) & 1u) gb[y * 32] = PB[y] & 0x8FFF8FFFu;
             }
             lds_put_board(buf, lane, PB);      // the start board in buf has been read out
-        } else {
-            transpose32(PB);
-            if (rb) {
+        } else if (rb) {
 #pragma unroll
-                for (int y = 0; y < 32; y++)
-                    if ((rb >> y) & 1u) __builtin_nontemporal_store(PB[y], &gb[y * 32]);
-            }
-            if (OBS) {      // bits 12-14 in use: add the goal colours bit-sliced
-                transpose32(PB);
-#pragma unroll
-                for (int w = 0; w < 2; w++) {
-                    const u32 white = obs_rw ? (gv[0][w] & gv[1][w] & gv[2][w]) : 0u;
-                    u32 cy = 0u;
-#pragma unroll
-                    for (int k = 0; k < 3; k++) {
-                        const u32 g = gv[k][w] & ~white, p = PL(PB, 12 + k, w);
-                        PL(PB, 12 + k, w) = p ^ g ^ cy;
-                        cy = maj(p, g, cy);
-                    }
-                    PL(PB, 15, w) ^= cy;
-                }
-                transpose32(PB);
-                lds_put_board(buf, lane, PB);
-            }
+            for (int y = 0; y < 32; y++)
+                if ((rb >> y) & 1u) __builtin_nontemporal_store(PB[y], &gb[y * 32]);
         }
     }
-    if (OBS) {
+    if (OBS && !hi) {
         __builtin_amdgcn_sched_barrier(0);
         write_obs(buf, fx, fl, b, lane);
         __builtin_amdgcn_sched_barrier(0);
@@ -655,6 +641,21 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         reset = epilogue_core(st, a, b, fl, act_reward, points, score, possible, side_total,
                               reward_out, done_out, flags_out, ep_len_out, ep_rew_out);
     reset = __builtin_amdgcn_readfirstlane(reset);
+    if (OBS && hi && !(fx.fuse_reset && reset)) {
+        // a board using bits 12-14 (no cell type does): the view from the stored state
+        // once everything has landed -- the action's writes, this step's goal and row
+        // stores and the epilogue's exit cells (this wave's own stores) -- as
+        // k_env_obs_packed computes it; an env reset after the step gets its view from
+        // the reset-list kernel instead
+        wait_vm();
+        const FastExtra &lfx = kernarg().fx;
+        sl::obs::ObsArgs oa{};
+        oa.vh = lfx.obs_vh;
+        oa.vw = lfx.obs_vw;
+        oa.remove_white = lfx.obs_rw;
+        oa.mode = SL_OBS_PACKED;
+        sl::obs::obs_packed_wave(st, oa, b, lane, lfx.obs_out);
+    }
     if (fx.fuse_reset && reset && lane == 0) {
         // queue the env for the reset kernel (k_env_reset_list)
         int64_t *cnt = fx.scratch + 8 * st.B + 2 + (a.step & 1);

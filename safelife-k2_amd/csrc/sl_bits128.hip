@@ -185,8 +185,12 @@ k_env_step_bits128(Step128KArgs ka) {
     __attribute__((address_space(3))) u32 *spool = (__attribute__((address_space(3))) u32 *)spool_;
     __shared__ uint16_t slots_[kDrawSlots];
     lds_u16 *slots = (lds_u16 *)slots_;
-    const int pok = rec(V, R_POK) & 6;
+    const int pok_all = rec(V, R_POK), pok = pok_all & 6;
+    int gok = pok;              // the goals' planes_ok bits after this step
     const Scratch w = scratch_of(fx.scratch, st.B);
+    // replay: the board's count mirror (planes 0, 4, 6, 7) is rewritten band by band
+    u32 *me = (MODE == SPAWN_STREAM && st.elig_planes) ? st.elig_planes + b * 2048 + lane
+                                                       : nullptr;
 
     SpawnCtx sc;
     sc.gid = a.env0 + (uint32_t)b;
@@ -243,8 +247,7 @@ k_env_step_bits128(Step128KArgs ka) {
             }
         }
         const bool fixed = changed == 0 && __ballot(spawners != 0u) == 0ull;
-        const int ok = 2 | (fixed ? 4 : 0);
-        if (ok != pok && lane == 0) st.planes_ok[b] = ok;
+        gok = 2 | (fixed ? 4 : 0);
         wait_vm();          // the mirror words are read back below
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -286,6 +289,14 @@ k_env_step_bits128(Step128KArgs ka) {
         rule_planes(P, cb, geo, sc, 0u);
         pos_b += geo.used;
         up = last;
+        if (MODE == SPAWN_STREAM && me) {
+#pragma unroll
+            for (int s = 0; s < 4; s++)
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+                    __builtin_nontemporal_store(PL(P, elig_plane(s), q),
+                                                &me[t * 512 + (2 * s + q) * 64]);
+        }
         __builtin_amdgcn_sched_barrier(0);
         u32 gcol[3][2];
         const u32 *m = mg + t * MW;
@@ -321,6 +332,10 @@ k_env_step_bits128(Step128KArgs ka) {
     }
     const int points = wave_total(pts), score = wave_total(scr);
     const int possible = wave_total(pos), side_total = wave_total(side);
+    // goals mirror bits, and bit 3 = the board count mirror is current (replay only:
+    // a Philox step clears it)
+    const int ok = gok | (me ? 8 : 0);
+    if (ok != pok_all && lane == 0) st.planes_ok[b] = ok;
     wait_vm();              // row stores land before the epilogue rewrites the exits
     if (lane == 0) {
         const Step128KArgs &k = kargs128();
@@ -340,7 +355,10 @@ k_env_step_bits128(Step128KArgs ka) {
 // act[] -- so the board read here is the acted-on one: the eligible cells of the board
 // and of the goals, band by band (scratch counts[2b], [2b+1]; sl_exclusive_scan_i64
 // turns them into each tensor's first uniform).  The work of k_env_count (sl_env.hip)
-// on the bit-sliced rule.
+// on the bit-sliced rule.  The board is counted from its count mirror when that is
+// current (planes_ok bit 3: the last step was a replay step and the action pre-pass
+// patched its edits in): 8 KiB of planes per env instead of the 32 KiB board, and no
+// transpose.
 __global__ void __launch_bounds__(64)
 k_stream_prologue128(Step128KArgs ka) {
     const sl_env_state &st = ka.st;
@@ -370,10 +388,46 @@ k_stream_prologue128(Step128KArgs ka) {
         }
         return wave_total(n);
     };
+    // the same count from the mirror's planes 0, 4, 6, 7 (the rest read as 0: they do
+    // not enter eligibility); a band's outside rows are bit 31 / bit 0 of the
+    // neighbouring bands' words
+    auto count_mirror = [&](const u32 *me) {
+        u32 M[NB][4][2];
+#pragma unroll
+        for (int t = 0; t < NB; t++)
+#pragma unroll
+            for (int s = 0; s < 4; s++)
+#pragma unroll
+                for (int q = 0; q < 2; q++) M[t][s][q] = me[t * 512 + (2 * s + q) * 64];
+        int n = 0;
+#pragma unroll
+        for (int t = 0; t < NB; t++) {
+            const int tu = (t + NB - 1) & (NB - 1), td = (t + 1) & (NB - 1);
+            u32 P[32], up = 0u, dn = 0u;
+#pragma unroll
+            for (int k = 0; k < 32; k++) P[k] = 0u;
+#pragma unroll
+            for (int s = 0; s < 4; s++)
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const int p = elig_plane(s);
+                    PL(P, p, q) = M[t][s][q];
+                    up |= (M[tu][s][q] >> 31) << (p + 16 * q);
+                    dn |= (M[td][s][q] & 1u) << (p + 16 * q);
+                }
+            GeoBand<SPAWN_COUNT> geo{lane, 32 * t, HaloView{up, dn}, none, 0, 0, 0, nullptr};
+            u32 ch[2];
+            rule_planes(P, ch, geo, sc, 0u);
+            n += geo.count;
+        }
+        return wave_total(n);
+    };
     // a board or goals without spawners (spawn_flags, set at reset: no rule or action
     // creates one) draws nothing; nor do goals at their fixed point (planes_ok bit 2)
     const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);     // toggling powers can make one
-    const int nb = (spf & 1) ? count(gb) : 0;
+    const bool mirror = st.elig_planes && (rec(V, R_POK) & 8);
+    const int nb = !(spf & 1) ? 0 : mirror ? count_mirror(st.elig_planes + b * 2048 + lane)
+                                           : count(gb);
     const int ng = ((rec(V, R_POK) & 6) == 6 || !(spf & 2)) ? 0 : count(gg);
     if (lane == 0) {
         w.counts[2 * b] = nb;

@@ -143,6 +143,20 @@ k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int 
                     cell_terms(bd[cells[k]], gd[cells[k]], sd[cells[k]], &p, &q, &se);
                     d_pts += p; d_scr += q; d_side += se;
                 }
+        // the 128x128 replay count mirror (sl_env_state.elig_planes) follows the edits
+        if (!DELTAS && st.elig_planes && H == 128 && W == 128 && (st.planes_ok[b] & 8))
+            for (int k = 0; k < 4; k++)
+                if (uniq[k]) {
+                    const int y = cells[k] >> 7, x = cells[k] & 127;
+                    const uint32_t v = bd[cells[k]], bit = 1u << (y & 31);
+                    uint32_t *m = st.elig_planes + b * 2048 + (y >> 5) * 512 + (x & 1) * 64 +
+                                  (x >> 1);
+                    for (int s = 0; s < 4; s++) {
+                        const int pl = elig_plane(s);
+                        const uint32_t old = m[s * 128];
+                        m[s * 128] = ((v >> pl) & 1u) ? (old | bit) : (old & ~bit);
+                    }
+                }
     }
     act[b] = reward;
     if (DELTAS) {

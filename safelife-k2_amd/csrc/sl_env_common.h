@@ -24,6 +24,10 @@ __host__ __device__ inline Scratch scratch_of(int64_t *s, int64_t B) {
 }
 __host__ __device__ inline int32_t *reset_list(int64_t *s) { return reinterpret_cast<int32_t *>(s); }
 
+// the board planes the 128x128 replay count mirror keeps (sl_env_state.elig_planes):
+// alive, frozen, inhibiting, spawning -- everything an eligible-cell count reads
+__host__ __device__ constexpr int elig_plane(int s) { return s == 0 ? 0 : (s == 1 ? 4 : s + 4); }
+
 struct StepArgs {
     int32_t time_limit, auto_reset, bonus_len, bonus_period;
     double penalty_coef;

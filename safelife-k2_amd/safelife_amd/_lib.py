@@ -42,7 +42,8 @@ class EnvState(ctypes.Structure):
                 ("prior_x", vp), ("prior_y", vp), ("prior_len", vp), ("prior_head", vp),
                 ("exit_count", vp), ("exit_y", vp), ("exit_x", vp),
                 ("level_index", vp), ("episodes", vp), ("num_steps", vp),
-                ("spawn_flags", vp), ("start_roll", vp), ("planes", vp), ("planes_ok", vp)]
+                ("spawn_flags", vp), ("start_roll", vp), ("planes", vp), ("planes_ok", vp),
+                ("elig_planes", vp)]
 
 
 class LevelPool(ctypes.Structure):

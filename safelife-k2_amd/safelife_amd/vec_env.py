@@ -160,6 +160,10 @@ class SafeLifeVecEnv:
             self.planes = z(B, H // 32, 32, 64)
             s.planes = self.planes.data_ptr()
             s.planes_ok = self.planes_ok.data_ptr()
+        if (H, W) == (128, 128) and self.rng == "stream":
+            # replay's count mirror of the board (planes 0, 4, 6, 7; 8 KiB per env)
+            self.elig_planes = z(B, 4, 4, 2, 64)
+            s.elig_planes = self.elig_planes.data_ptr()
         self._state = s
         self.actions_dev = z(B)
         self.reward = z(B, dt=torch.float64)
@@ -451,7 +455,7 @@ class SafeLifeVecEnv:
         return s
 
     def _state_tensor(self, name):
-        if name in ("board", "goals", "start_board", "planes", "planes_ok"):
+        if name in ("board", "goals", "start_board", "planes", "planes_ok", "elig_planes"):
             return getattr(self, name)
         return self.st_t[name]
 
