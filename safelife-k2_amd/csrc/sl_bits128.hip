@@ -399,6 +399,24 @@ k_stream_prologue128(Step128KArgs ka) {
             for (int s = 0; s < 4; s++)
 #pragma unroll
                 for (int q = 0; q < 2; q++) M[t][s][q] = me[t * 512 + (2 * s + q) * 64];
+        // the rows the action pre-pass may have edited since the mirror was written
+        // (scratch act[B + b], bytes 0xFF = none): re-read from the board
+        const u32 rows = (u32)w.act[st.B + b];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const u32 y = (rows >> (8 * j)) & 0xFFu;
+            if (y >= (u32)N) continue;                  // wave-uniform
+            const u32 d = gb[y * RS], bit = 1u << (y & 31);
+#pragma unroll
+            for (int t = 0; t < NB; t++)
+                if ((int)(y >> 5) == t)
+#pragma unroll
+                    for (int s = 0; s < 4; s++)
+#pragma unroll
+                        for (int q = 0; q < 2; q++)
+                            M[t][s][q] = ((d >> (elig_plane(s) + 16 * q)) & 1u)
+                                             ? (M[t][s][q] | bit) : (M[t][s][q] & ~bit);
+        }
         int n = 0;
 #pragma unroll
         for (int t = 0; t < NB; t++) {

@@ -65,6 +65,7 @@ k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int 
     uint16_t *bd = st.board + b * hw;
     const uint16_t *gd = st.goals + b * hw, *sd = st.start_board + b * hw;
     int reward = 0, d_pts = 0, d_scr = 0, d_side = 0;
+    uint32_t edit_rows = 0xFFFFFFFFu;      // rows the action may have edited (0xFF: none)
     const int a = actions[b];
     if (!st.game_over[b] && a >= 1 && a <= 8) {
         const int orient = (a - 1) & 3;
@@ -143,22 +144,21 @@ k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int 
                     cell_terms(bd[cells[k]], gd[cells[k]], sd[cells[k]], &p, &q, &se);
                     d_pts += p; d_scr += q; d_side += se;
                 }
-        // the 128x128 replay count mirror (sl_env_state.elig_planes) follows the edits
-        if (!DELTAS && st.elig_planes && H == 128 && W == 128 && (st.planes_ok[b] & 8))
-            for (int k = 0; k < 4; k++)
-                if (uniq[k]) {
-                    const int y = cells[k] >> 7, x = cells[k] & 127;
-                    const uint32_t v = bd[cells[k]], bit = 1u << (y & 31);
-                    uint32_t *m = st.elig_planes + b * 2048 + (y >> 5) * 512 + (x & 1) * 64 +
-                                  (x >> 1);
-                    for (int s = 0; s < 4; s++) {
-                        const int pl = elig_plane(s);
-                        const uint32_t old = m[s * 128];
-                        m[s * 128] = ((v >> pl) & 1u) ? (old | bit) : (old & ~bit);
-                    }
-                }
+        // the 128x128 replay count mirror (sl_env_state.elig_planes) is behind by the
+        // rows of these cells: the count prologue re-reads them from the board
+        if (!DELTAS && st.elig_planes && H == 128 && W == 128) {
+            uint32_t rows = 0xFFFFFFFFu;
+            for (int k = 0; k < 4; k++) {
+                const uint32_t y = (uint32_t)(cells[k] >> 7);
+                bool seen = false;
+                for (int j = 0; j < 4; j++) seen = seen || ((rows >> (8 * j)) & 0xFFu) == y;
+                if (!seen) rows = (rows << 8) | y;
+            }
+            edit_rows = rows;
+        }
     }
     act[b] = reward;
+    if (!DELTAS && st.elig_planes) act[st.B + b] = (int64_t)edit_rows;
     if (DELTAS) {
         act[st.B + b] = d_pts;
         act[2 * st.B + b] = d_scr;
