@@ -223,18 +223,23 @@ typedef struct sl_env_state {
                                  bit 1 is set.                                 */
     int32_t *planes_ok;       /* [B] bit1: goals mirror valid; bit2: goals at
                                  a fixed point (no spawner, unchanged by the
-                                 last step: the rule is skipped); bit3: board
-                                 count mirror (elig_planes) valid.  Anything
+                                 last step: the rule is skipped); bit3: the
+                                 board's draw planes (elig_planes) hold its
+                                 eligible cells as the last step left them.
+                                 Anything
                                  that writes the goals other than the 64x64
                                  kernel and its reset clears it.               */
-    uint32_t *elig_planes;    /* replay mode, 128x128: the board's planes 0, 4,
-                                 6, 7 (alive, frozen, inhibiting, spawning) --
-                                 all an eligible-cell count reads -- written by
-                                 the replay step, patched by the action pre-pass,
-                                 read by the next step's count (8 KiB per env
-                                 instead of the 32 KiB board):
-                                 [B][band t][s][word w][lane], s = 0..3 for
-                                 planes 0, 4, 6, 7; or NULL                     */
+    uint32_t *elig_planes;    /* replay mode, 128x128, [B][1024] words: the
+                                 draw planes [tensor][band t][word w][lane] (bit
+                                 y of word w of lane j = cell (32t + y, 2j + w)).
+                                 The step kernel leaves the advanced board's
+                                 eligible cells in tensor 0's (planes_ok bit 3);
+                                 the next step's count patches the rows its
+                                 action edited and counts them; the draw pass
+                                 replaces each drawing tensor's eligible cells
+                                 with those whose uniforms spawn, before the
+                                 step kernel runs.  Or NULL (the step kernel
+                                 then ranks and draws itself)                  */
 } sl_env_state;
 
 /* A device-resident level pool (the level_iterator's levels). */

@@ -146,8 +146,10 @@ struct SpawnCtx {
 //   SPAWN_STREAM  the reference's order (SL_RNG_STREAM): a tensor's eligible cells take
 //                 consecutive uniforms of a supplied stream, row-major (stream_draws);
 //   SPAWN_COUNT   no draws: only count the eligible cells (the replay prologue kernels
-//                 that size each tensor's slice of the stream).
-enum : int { SPAWN_PHILOX = 0, SPAWN_STREAM = 1, SPAWN_COUNT = 2 };
+//                 that size each tensor's slice of the stream);
+//   SPAWN_DECIDED the reference's order, drawn before the step by a kernel of its own
+//                 (128x128: k_stream_draw128): the geometry holds the spawning cells.
+enum : int { SPAWN_PHILOX = 0, SPAWN_STREAM = 1, SPAWN_COUNT = 2, SPAWN_DECIDED = 3 };
 
 // the supplied stream (StepArgs draws / n_draws) and the error word (scratch[8B])
 struct StreamSrc {

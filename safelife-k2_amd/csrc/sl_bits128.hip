@@ -73,6 +73,8 @@ struct GeoBand {
     int used;
     int count;         // SPAWN_COUNT: this lane's eligible cells
     lds_u16 *slots;    // SPAWN_PHILOX: compact_draws' queue (kDrawSlots)
+    u32 e[2];          // SPAWN_COUNT: the band's eligible cells; SPAWN_DECIDED: the
+                       // cells k_stream_draw128 decided spawn
     template <class F>
     __device__ __forceinline__ V3 vert(const u32 *P, int w, F f) const {
         return vert_with(f(P, w), f(hv, w));
@@ -96,8 +98,13 @@ struct GeoBand {
             philox_spawn_compact(*this, elig, sp, sc, tensor, slots);
         } else if (MODE == SPAWN_STREAM) {
             used = stream_draws<false>(elig, sp, sc.thr, src, pos, lane);
+        } else if (MODE == SPAWN_DECIDED) {
+            sp[0] = elig[0] & e[0];
+            sp[1] = elig[1] & e[1];
         } else {
             count += __builtin_popcount(elig[0]) + __builtin_popcount(elig[1]);
+            e[0] = elig[0];
+            e[1] = elig[1];
         }
     }
 };
@@ -143,6 +150,52 @@ __device__ __forceinline__ void pool_start_lds(const __attribute__((address_spac
     }
 }
 
+// the decided spawns of band t of a tensor (0 board, 1 goals) for the step kernel's
+// rule: loaded at the band's start, under its row loads; none when the tensor draws
+// nothing this step (`draws` false)
+template <class G>
+__device__ __forceinline__ void draw_planes(G &geo, const u32 *me, int tensor, int t, bool draws) {
+    geo.e[0] = geo.e[1] = 0u;
+    if (draws) {
+        const u32 *d = me + kDrawPlanes + (tensor * NB + t) * 128;
+        geo.e[0] = d[0];
+        geo.e[1] = d[64];
+    }
+}
+
+// Row y of eligibility planes pl (planes 0, 4, 6, 7 x 2 words, elig_plane) as a row
+// dword (bit p + 16 w = plane p of column 2 lane + w), the form HaloView takes.
+__device__ __forceinline__ u32 pack_row(const u32 pl[8], int y) {
+    u32 d = 0u;
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+        for (int q = 0; q < 2; q++) d |= ((pl[2 * s + q] >> y) & 1u) << (elig_plane(s) + 16 * q);
+    return d;
+}
+
+// The eligible cells of band t of the advanced board -- the next step's spawn
+// eligibility before its action -- from the band's planes 0, 4, 6, 7 and the
+// neighbouring rows up / dn (row dwords); the rest of the rule folds away.  Stored as
+// the board's draw planes, which k_stream_prologue128 patches and counts.
+__device__ __forceinline__ void next_elig(const u32 pl[8], u32 up, u32 dn, int t, int lane,
+                                          u32 *me) {
+    u32 P[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) P[k] = 0u;
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+        for (int q = 0; q < 2; q++) PL(P, elig_plane(s), q) = pl[2 * s + q];
+    const StreamSrc none{nullptr, 0, nullptr};
+    const SpawnCtx sc{0u, 0u, 0ull, 0.0};
+    GeoBand<SPAWN_COUNT> geo{lane, 32 * t, HaloView{up, dn}, none, 0, 0, 0, nullptr};
+    u32 ch[2];
+    rule_planes(P, ch, geo, sc, 0u);
+    __builtin_nontemporal_store(geo.e[0], &me[kDrawPlanes + t * 128]);
+    __builtin_nontemporal_store(geo.e[1], &me[kDrawPlanes + t * 128 + 64]);
+}
+
 // all kernel arguments in one struct at kernarg offset 0: the epilogue re-reads its
 // pointers where it runs (kargs128()), so they are not held in SGPRs through the bands
 struct Step128KArgs {
@@ -164,8 +217,9 @@ __device__ __forceinline__ const Step128KArgs &kargs128() {
 
 // One env-step of env b, after the action: k_env_action has applied it -- state and cell edits in HBM, reward
 // in scratch act[b] -- so this kernel holds no action code, no edit lists and no
-// overlay.  MODE: SPAWN_PHILOX, or SPAWN_STREAM (each tensor's first uniform from the
-// scratch offsets).
+// overlay.  MODE: SPAWN_PHILOX; SPAWN_STREAM (each tensor's first uniform from the
+// scratch offsets); or SPAWN_DECIDED (the spawns from the draw planes k_stream_draw128
+// left, replay with sl_env_state.elig_planes).
 template <int MODE>
 __global__ void __launch_bounds__(64, kMinWaves)
 k_env_step_bits128(Step128KArgs ka) {
@@ -188,9 +242,11 @@ k_env_step_bits128(Step128KArgs ka) {
     const int pok_all = rec(V, R_POK), pok = pok_all & 6;
     int gok = pok;              // the goals' planes_ok bits after this step
     const Scratch w = scratch_of(fx.scratch, st.B);
-    // replay: the board's count mirror (planes 0, 4, 6, 7) is rewritten band by band
-    u32 *me = (MODE == SPAWN_STREAM && st.elig_planes) ? st.elig_planes + b * 2048 + lane
-                                                       : nullptr;
+    // replay with draw planes: the spawns come decided from them (k_stream_draw128), for
+    // the tensors that draw (scratch act[B + b] bit 0 board, bit 1 goals), and the
+    // advanced board's eligible cells go back into the board's planes
+    u32 *me = MODE == SPAWN_DECIDED ? st.elig_planes + b * kEligStride + lane : nullptr;
+    const int dfl = MODE == SPAWN_DECIDED ? (int)w.act[st.B + b] : 0;
 
     SpawnCtx sc;
     sc.gid = a.env0 + (uint32_t)b;
@@ -225,6 +281,7 @@ k_env_step_bits128(Step128KArgs ka) {
             transpose32(G);
             u32 cg[2];
             GeoBand<MODE> geo{lane, 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_g, 0, 0, slots};
+            if (MODE == SPAWN_DECIDED) draw_planes(geo, me, 1, t, dfl & 2);
             rule_planes(G, cg, geo, sc, 1u);
             pos_g += geo.used;
             up = last;
@@ -272,6 +329,12 @@ k_env_step_bits128(Step128KArgs ka) {
     const int sc0 = (2 * lane - sdx) & (N - 1), sc1 = (sc0 + 1) & (N - 1);
     int pts = 0, scr = 0, pos = 0, side = 0;
     u32 up = gb[(N - 1) * RS], row0 = 0;
+    // SPAWN_DECIDED: the eligibility planes of the previous band (of band 0 in LDS, in
+    // the draw slots this mode does not use), the advanced row 31 of the band before
+    // that and row 0 of band 1: band t - 1's next eligibility is evaluated once band t
+    // has advanced, bands 3 and 0 after the loop
+    __attribute__((address_space(3))) u32 *e0 = (__attribute__((address_space(3))) u32 *)slots_;
+    u32 EP[8], r31 = 0u, d1 = 0u;
 #pragma unroll 1
     for (int t = 0; t < NB; t++) {
         u32 P[32];
@@ -286,16 +349,24 @@ k_env_step_bits128(Step128KArgs ka) {
         transpose32(P);
         u32 cb[2];
         GeoBand<MODE> geo{lane, 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_b, 0, 0, slots};
+        if (MODE == SPAWN_DECIDED) draw_planes(geo, me, 0, t, dfl & 1);
         rule_planes(P, cb, geo, sc, 0u);
         pos_b += geo.used;
         up = last;
-        if (MODE == SPAWN_STREAM && me) {
+        if (MODE == SPAWN_DECIDED) {
+            u32 EC[8];
 #pragma unroll
             for (int s = 0; s < 4; s++)
 #pragma unroll
-                for (int q = 0; q < 2; q++)
-                    __builtin_nontemporal_store(PL(P, elig_plane(s), q),
-                                                &me[t * 512 + (2 * s + q) * 64]);
+                for (int q = 0; q < 2; q++) EC[2 * s + q] = PL(P, elig_plane(s), q);
+            if (t >= 2) next_elig(EP, r31, pack_row(EC, 0), t - 1, lane, me);
+            if (t == 1) d1 = pack_row(EC, 0);
+            if (t >= 1) r31 = pack_row(EP, 31);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if (t == 0) e0[k * 64 + lane] = EC[k];
+                EP[k] = EC[k];
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
         u32 gcol[3][2];
@@ -330,10 +401,17 @@ k_env_step_bits128(Step128KArgs ka) {
                 if ((rb >> y) & 1u) __builtin_nontemporal_store(P[y], &gb[(32 * t + y) * RS]);
         }
     }
+    if (MODE == SPAWN_DECIDED) {
+        u32 E0[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) E0[k] = e0[k * 64 + lane];
+        next_elig(EP, r31, pack_row(E0, 0), NB - 1, lane, me);
+        next_elig(E0, pack_row(EP, 31), d1, 0, lane, me);
+    }
     const int points = wave_total(pts), score = wave_total(scr);
     const int possible = wave_total(pos), side_total = wave_total(side);
-    // goals mirror bits, and bit 3 = the board count mirror is current (replay only:
-    // a Philox step clears it)
+    // goals mirror bits, and bit 3 = the board's draw planes hold the advanced board's
+    // eligible cells (decided replay only: any other step clears it)
     const int ok = gok | (me ? 8 : 0);
     if (ok != pok_all && lane == 0) st.planes_ok[b] = ok;
     wait_vm();              // row stores land before the epilogue rewrites the exits
@@ -355,10 +433,9 @@ k_env_step_bits128(Step128KArgs ka) {
 // act[] -- so the board read here is the acted-on one: the eligible cells of the board
 // and of the goals, band by band (scratch counts[2b], [2b+1]; sl_exclusive_scan_i64
 // turns them into each tensor's first uniform).  The work of k_env_count (sl_env.hip)
-// on the bit-sliced rule.  The board is counted from its count mirror when that is
-// current (planes_ok bit 3: the last step was a replay step and the action pre-pass
-// patched its edits in): 8 KiB of planes per env instead of the 32 KiB board, and no
-// transpose.
+// on the bit-sliced rule.  When the last step was a decided replay step (planes_ok
+// bit 3) the board's eligible cells are already in its draw planes, bar the rows the
+// action edited: 2 KiB per env and a few board rows instead of the 32 KiB board.
 __global__ void __launch_bounds__(64)
 k_stream_prologue128(Step128KArgs ka) {
     const sl_env_state &st = ka.st;
@@ -371,8 +448,16 @@ k_stream_prologue128(Step128KArgs ka) {
     const Scratch w = scratch_of(ka.fx.scratch, st.B);
     SpawnCtx sc{0u, 0u, 0ull, 0.0};
     const StreamSrc none{nullptr, 0, nullptr};
+    // the draw planes: each counted tensor's eligible cells, for k_stream_draw128
+    u32 *dp = st.elig_planes ? st.elig_planes + b * kEligStride + kDrawPlanes + lane : nullptr;
+    auto keep = [&](const GeoBand<SPAWN_COUNT> &geo, int tensor, int t) {
+        if (dp) {
+            dp[(tensor * NB + t) * 128] = geo.e[0];
+            dp[(tensor * NB + t) * 128 + 64] = geo.e[1];
+        }
+    };
     // the eligible cells of one tensor, band by band
-    auto count = [&](const u32 *g) {
+    auto count = [&](const u32 *g, int tensor) {
         int n = 0;
 #pragma unroll 1
         for (int t = 0; t < NB; t++) {
@@ -385,71 +470,247 @@ k_stream_prologue128(Step128KArgs ka) {
             u32 ch[2];
             rule_planes(P, ch, geo, sc, 0u);
             n += geo.count;
+            keep(geo, tensor, t);
         }
         return wave_total(n);
     };
-    // the same count from the mirror's planes 0, 4, 6, 7 (the rest read as 0: they do
-    // not enter eligibility); a band's outside rows are bit 31 / bit 0 of the
-    // neighbouring bands' words
-    auto count_mirror = [&](const u32 *me) {
-        u32 M[NB][4][2];
+    // the same count from the eligible cells the last (replay) step left in the board's
+    // draw planes, with the rows the action pre-pass may have edited (scratch
+    // act[B + b], bytes 0xFF = none; all within rows agent - 1 .. agent + 2) and their
+    // neighbours re-evaluated: the board rows around them are loaded into one 32-row
+    // window, the edited rows at 2..29 of it, and the window's eligibility replaces
+    // rows y - 1 .. y + 1 of each edited row y.  Returns -1 when the edited rows do not
+    // fit one window (the full count then runs).
+    auto count_next = [&]() -> int {
+        u32 E[NB][2];
 #pragma unroll
         for (int t = 0; t < NB; t++)
 #pragma unroll
-            for (int s = 0; s < 4; s++)
-#pragma unroll
-                for (int q = 0; q < 2; q++) M[t][s][q] = me[t * 512 + (2 * s + q) * 64];
-        // the rows the action pre-pass may have edited since the mirror was written
-        // (scratch act[B + b], bytes 0xFF = none): re-read from the board
+            for (int q = 0; q < 2; q++) E[t][q] = dp[t * 128 + 64 * q];
         const u32 rows = (u32)w.act[st.B + b];
+        int y0 = -1, dmin = 0, dmax = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const u32 y = (rows >> (8 * j)) & 0xFFu;
-            if (y >= (u32)N) continue;                  // wave-uniform
-            const u32 d = gb[y * RS], bit = 1u << (y & 31);
+            const int y = (int)((rows >> (8 * j)) & 0xFFu);
+            if (y >= N) continue;                       // wave-uniform
+            if (y0 < 0) y0 = y;
+            const int d = ((y - y0 + N / 2) & (N - 1)) - N / 2;
+            dmin = min(dmin, d);
+            dmax = max(dmax, d);
+        }
+        if (y0 >= 0) {
+            if (dmax - dmin > 27) return -1;
+            const int base = (y0 + dmin - 2) & (N - 1), nrows = dmax - dmin + 5;
+            u32 P[32];
+#pragma unroll
+            for (int i = 0; i < 32; i++) P[i] = i < nrows ? gb[((base + i) & (N - 1)) * RS] : 0u;
+            transpose32(P);
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                if (k != 0 && k != 4 && k != 6 && k != 7) PL(P, k, 0) = PL(P, k, 1) = 0u;
+            GeoBand<SPAWN_COUNT> geo{lane, 0, HaloView{0u, 0u}, none, 0, 0, 0, nullptr};
+            u32 ch[2];
+            rule_planes(P, ch, geo, sc, 0u);
+            u32 rm = 0u;                                // window rows re-evaluated
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int y = (int)((rows >> (8 * j)) & 0xFFu);
+                if (y < N) rm |= 7u << (((y - base) & (N - 1)) - 1);
+            }
+            const int sh = base & 31, tb = base >> 5;
 #pragma unroll
             for (int t = 0; t < NB; t++)
-                if ((int)(y >> 5) == t)
 #pragma unroll
-                    for (int s = 0; s < 4; s++)
-#pragma unroll
-                        for (int q = 0; q < 2; q++)
-                            M[t][s][q] = ((d >> (elig_plane(s) + 16 * q)) & 1u)
-                                             ? (M[t][s][q] | bit) : (M[t][s][q] & ~bit);
+                for (int q = 0; q < 2; q++) {
+                    if (t == tb)
+                        E[t][q] = (E[t][q] & ~(rm << sh)) | ((geo.e[q] & rm) << sh);
+                    if (sh && t == ((tb + 1) & (NB - 1)))
+                        E[t][q] = (E[t][q] & ~(rm >> (32 - sh))) | ((geo.e[q] & rm) >> (32 - sh));
+                }
         }
         int n = 0;
 #pragma unroll
-        for (int t = 0; t < NB; t++) {
-            const int tu = (t + NB - 1) & (NB - 1), td = (t + 1) & (NB - 1);
-            u32 P[32], up = 0u, dn = 0u;
+        for (int t = 0; t < NB; t++)
 #pragma unroll
-            for (int k = 0; k < 32; k++) P[k] = 0u;
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    const int p = elig_plane(s);
-                    PL(P, p, q) = M[t][s][q];
-                    up |= (M[tu][s][q] >> 31) << (p + 16 * q);
-                    dn |= (M[td][s][q] & 1u) << (p + 16 * q);
-                }
-            GeoBand<SPAWN_COUNT> geo{lane, 32 * t, HaloView{up, dn}, none, 0, 0, 0, nullptr};
-            u32 ch[2];
-            rule_planes(P, ch, geo, sc, 0u);
-            n += geo.count;
-        }
+            for (int q = 0; q < 2; q++) {
+                n += __builtin_popcount(E[t][q]);
+                dp[t * 128 + 64 * q] = E[t][q];
+            }
         return wave_total(n);
     };
     // a board or goals without spawners (spawn_flags, set at reset: no rule or action
     // creates one) draws nothing; nor do goals at their fixed point (planes_ok bit 2)
     const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);     // toggling powers can make one
-    const bool mirror = st.elig_planes && (rec(V, R_POK) & 8);
-    const int nb = !(spf & 1) ? 0 : mirror ? count_mirror(st.elig_planes + b * 2048 + lane)
-                                           : count(gb);
-    const int ng = ((rec(V, R_POK) & 6) == 6 || !(spf & 2)) ? 0 : count(gg);
+    const bool next = st.elig_planes && (rec(V, R_POK) & 8);
+    int nb = 0;
+    if (spf & 1) {
+        nb = next ? count_next() : -1;
+        if (nb < 0) nb = count(gb, 0);
+    }
+    const int ng = ((rec(V, R_POK) & 6) == 6 || !(spf & 2)) ? 0 : count(gg, 1);
     if (lane == 0) {
         w.counts[2 * b] = nb;
         w.counts[2 * b + 1] = ng;
+        // the tensors that draw, for k_stream_draw128 and the step (the action's edited
+        // rows in this slot have been read)
+        if (dp) w.act[st.B + b] = (nb ? 1 : 0) | (ng ? 2 : 0);
+    }
+}
+
+// The two 32x32 bit matrices held by lanes 0-31 and 32-63, transposed within each
+// half (bit y of lane i's word -> bit i of lane y's word): five block-swap stages,
+// the partner word (lane ^ s) from ds_swizzle, the swapped block by a rotation and a
+// bitfield insert.
+template <int S, u32 M>
+__device__ __forceinline__ u32 swap_stage(u32 x, int lane) {
+    const bool hi = (lane & S) != 0;
+    const u32 p = (u32)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (S << 10));
+    const u32 sh = __builtin_amdgcn_alignbit(p, p, hi ? S : 32 - S);     // rotate
+    const u32 mm = hi ? ~M : M;
+    return (x & mm) | (sh & ~mm);
+}
+__device__ __forceinline__ u32 transpose_halves(u32 x, int lane) {
+    x = swap_stage<16, 0x0000FFFFu>(x, lane);
+    x = swap_stage<8, 0x00FF00FFu>(x, lane);
+    x = swap_stage<4, 0x0F0F0F0Fu>(x, lane);
+    x = swap_stage<2, 0x33333333u>(x, lane);
+    return swap_stage<1, 0x55555555u>(x, lane);
+}
+
+// inclusive sum over the lanes of each 32-lane half
+__device__ __forceinline__ int scan_halves(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);     // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);     // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);     // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);     // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);    // row_bcast:15
+    return v;
+}
+
+// Replay-mode draws of env b, after the offsets scan: each drawing tensor's eligible
+// cells (the draw planes, from k_stream_prologue128) take the uniforms from its
+// offset on in row-major order, one per eligible cell (random.c:47-52 consumed by
+// advance_board.c:109-113), and the cells that spawn replace them in the draw planes.
+// The step kernel then only ANDs them into its spawns.  Ranks without a pass per row:
+//  * each band's two words are transposed across the lanes (transpose_halves): lane
+//    32k + r then holds row r's cells of lanes 32k..32k+31 -- a "segment" of 64
+//    cells, in the stream's order; segments run (band, row, half);
+//  * segment sizes by popcount, their bases by a scan over the rows (DPP) and the
+//    band totals, into LDS with the segment's two words;
+//  * lane i takes the ranks i, i + 64, ...: the segment by binary search over the
+//    bases, the cell by binary search over popcounts within it; the uniforms
+//    draws[pos + i] are contiguous (each load instruction one coalesced 512-byte run,
+//    kDrawBatch in flight per lane), and a spawn is ORed into the owner's word in LDS.
+// VALU work per tensor is a few hundred instructions, against ~2000 for a ballot per
+// eligible row.
+constexpr int kDrawBatch = 8;
+constexpr int kSegs = NB * 64;
+__global__ void __launch_bounds__(64)
+k_stream_draw128(Step128KArgs ka) {
+    const sl_env_state &st = ka.st;
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const Scratch w = scratch_of(ka.fx.scratch, st.B);
+    const int dfl = (int)w.act[st.B + b];
+    if (!(dfl & 3)) return;
+    __shared__ u32 segb_[kSegs];
+    __shared__ u32 segr_[2 * kSegs];   // [segment][word]
+    __shared__ u32 spw_[NB * 2 * 64];
+    typedef __attribute__((address_space(3))) u32 lds_u32;
+    lds_u32 *segb = (lds_u32 *)segb_;
+    lds_u32 *segr = (lds_u32 *)segr_;
+    lds_u32 *spw = (lds_u32 *)spw_;
+    const double thr = (double)st.spawn_prob[b];
+    const double *draws = ka.a.draws;
+    const int64_t n_draws = ka.a.n_draws;
+    u32 *dp = st.elig_planes + b * kEligStride + kDrawPlanes + lane;
+#pragma unroll 1
+    for (int tensor = 0; tensor < 2; tensor++) {
+        if (!((dfl >> tensor) & 1)) continue;
+        u32 E[NB][2];
+#pragma unroll
+        for (int t = 0; t < NB; t++)
+#pragma unroll
+            for (int q = 0; q < 2; q++) E[t][q] = dp[(tensor * NB + t) * 128 + 64 * q];
+        if (thr <= 0.0 || thr >= 1.0) {        // consumed, never compared (stream_draws)
+#pragma unroll
+            for (int t = 0; t < NB; t++)
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+                    dp[(tensor * NB + t) * 128 + 64 * q] = thr >= 1.0 ? E[t][q] : 0u;
+            continue;
+        }
+        const int64_t pos = w.offsets[2 * b + tensor];
+        // the segments: bases and cells
+        int total = 0;
+        const int half = lane >> 5;
+#pragma unroll
+        for (int t = 0; t < NB; t++) {
+            const u32 R0 = transpose_halves(E[t][0], lane), R1 = transpose_halves(E[t][1], lane);
+            const int c = __builtin_popcount(R0) + __builtin_popcount(R1);
+            const int cp = __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, c);
+            const int rc = c + cp;                      // the row's cells (both halves)
+            const int incl = scan_halves(rc);
+            const int seg = t * 64 + (lane & 31) * 2 + half;
+            segb[seg] = (u32)(total + incl - rc + (half ? cp : 0));
+            segr[2 * seg] = R0;
+            segr[2 * seg + 1] = R1;
+            total += __builtin_amdgcn_readlane(incl, 31);
+        }
+#pragma unroll
+        for (int k = 0; k < NB * 2; k++) spw[k * 64 + lane] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+        for (int i0 = 0; i0 < total; i0 += 64 * kDrawBatch) {
+            double u[kDrawBatch];
+            u32 cell[kDrawBatch];
+#pragma unroll
+            for (int k = 0; k < kDrawBatch; k++) {
+                const int i = i0 + 64 * k + lane;
+                u[k] = 1.0;
+                cell[k] = 0u;
+                if (i < total) {
+                    int sg = 0;                         // the last segment based at <= i
+#pragma unroll
+                    for (int step = kSegs / 2; step >= 1; step >>= 1)
+                        if ((int)segb[sg + step] <= i) sg += step;
+                    const u32 Rx = segr[2 * sg], Ry = segr[2 * sg + 1];
+                    int kk = i - (int)segb[sg], at = 0;  // the kk-th cell of the segment
+#pragma unroll
+                    for (int step = 16; step >= 1; step >>= 1) {
+                        const u32 msk = (1u << step) - 1u;
+                        const int cl = __builtin_popcount((Rx >> at) & msk) +
+                                       __builtin_popcount((Ry >> at) & msk);
+                        if (kk >= cl) {
+                            kk -= cl;
+                            at += step;
+                        }
+                    }
+                    const u32 q = (kk == 0 && ((Rx >> at) & 1u)) ? 0u : 1u;
+                    const u32 t = (u32)sg >> 6, row = ((u32)sg >> 1) & 31u;
+                    const u32 j = 32u * ((u32)sg & 1u) + (u32)at;
+                    cell[k] = (((t * 2 + q) * 64 + j) << 5) | row;
+                    const int64_t r = pos + i;
+                    if (r < n_draws) u[k] = draws[r];
+                    else atomicOr((unsigned long long *)w.err, 1ull);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kDrawBatch; k++)
+                if (u[k] < thr)
+                    __hip_atomic_fetch_or(&spw[cell[k] >> 5], 1u << (cell[k] & 31u),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int t = 0; t < NB; t++)
+#pragma unroll
+            for (int q = 0; q < 2; q++)
+                dp[(tensor * NB + t) * 128 + 64 * q] = spw[(t * 2 + q) * 64 + lane] & E[t][q];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // before the next tensor's
+        __builtin_amdgcn_wave_barrier();                        // segment writes
     }
 }
 
@@ -476,8 +737,15 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
         }
         const int rc = stream_offsets(st, fx, s);
         if (rc || !stream_steps(fx)) return rc;
-        if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        hipLaunchKernelGGL(k_env_step_bits128<SPAWN_STREAM>, grid, dim3(64), 0, s, ka);
+        if (st.elig_planes) {       // draws decided up front
+            hipLaunchKernelGGL(k_stream_draw128, grid, dim3(64), 0, s, ka);
+            if (hipGetLastError() != hipSuccess) return SL_EHIP;
+            if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
+            hipLaunchKernelGGL(k_env_step_bits128<SPAWN_DECIDED>, grid, dim3(64), 0, s, ka);
+        } else {
+            if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
+            hipLaunchKernelGGL(k_env_step_bits128<SPAWN_STREAM>, grid, dim3(64), 0, s, ka);
+        }
     } else {
         const int rc = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
         if (rc) return rc;

@@ -1211,7 +1211,8 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
 }
 
 // ---------------------------------------------------------------------------
-// trajectory capture (sl_capture): one block per captured env, 16-byte copies
+// trajectory capture (sl_capture): one block per captured env, one uint16 cell per
+// thread per iteration (a few envs per step: not worth vector copies)
 // ---------------------------------------------------------------------------
 namespace {
 __global__ void __launch_bounds__(NT)

@@ -12,7 +12,8 @@ namespace sl {
 //   [2B, 4B)  per-(env, tensor) stream offsets   (replay mode)
 //   [4B, 8B)  per env: action reward, d_points, d_score, d_side of the action's
 //             cell edits (the generic path; the bit-sliced replay prologues write
-//             the reward only)
+//             the reward only; 128x128 replay with elig_planes: [B, 2B) holds the
+//             rows the action edited, then the tensors that draw, bit0 board, bit1 goals)
 //   [8B]      error flags (bit0: draw stream exhausted)
 //   [8B+2], [8B+3]  reset-list lengths for even / odd steps (each step's reset
 //             kernel zeroes the other one)
@@ -24,9 +25,16 @@ __host__ __device__ inline Scratch scratch_of(int64_t *s, int64_t B) {
 }
 __host__ __device__ inline int32_t *reset_list(int64_t *s) { return reinterpret_cast<int32_t *>(s); }
 
-// the board planes the 128x128 replay count mirror keeps (sl_env_state.elig_planes):
-// alive, frozen, inhibiting, spawning -- everything an eligible-cell count reads
+// the board planes a cell's spawn eligibility reads (alive, frozen, inhibiting,
+// spawning): what the 128x128 replay paths evaluate eligibility from
 __host__ __device__ constexpr int elig_plane(int s) { return s == 0 ? 0 : (s == 1 ? 4 : s + 4); }
+// sl_env_state.elig_planes per env (u32 words): the draw planes
+// [tensor][band][word][lane] of the 128x128 replay.  The step kernel leaves the
+// eligible cells of its advanced board in tensor 0's planes (the next step's
+// eligibility before the action); k_stream_prologue128 patches the rows the action
+// edited, counts, and leaves each drawing tensor's eligible cells there;
+// k_stream_draw128 replaces them with the cells that spawn; the step kernel reads those
+constexpr int kEligStride = 1024, kDrawPlanes = 0;
 
 struct StepArgs {
     int32_t time_limit, auto_reset, bonus_len, bonus_period;

@@ -161,8 +161,9 @@ class SafeLifeVecEnv:
             s.planes = self.planes.data_ptr()
             s.planes_ok = self.planes_ok.data_ptr()
         if (H, W) == (128, 128) and self.rng == "stream":
-            # replay's count mirror of the board (planes 0, 4, 6, 7; 8 KiB per env)
-            self.elig_planes = z(B, 4, 4, 2, 64)
+            # replay's draw planes: each tensor's eligible cells, then its decided
+            # spawns (4 KiB per env)
+            self.elig_planes = z(B, 1024)
             s.elig_planes = self.elig_planes.data_ptr()
         self._state = s
         self.actions_dev = z(B)
@@ -500,12 +501,14 @@ class SafeLifeVecEnv:
         return d
 
     def load_state_dict(self, d):
-        """Restore a state_dict().  Level indices must address the current pool
-        (the start boards themselves are restored from the dict and read from HBM)."""
+        """Restore a state_dict().  The start boards are restored from the dict and
+        read from HBM (start_roll = -1), so level_index is informational: a snapshot
+        taken before a swap to a smaller pool restores, with a warning."""
         li = d["level_index"]
         if int(li.min().item()) < 0 or int(li.max().item()) >= self.pool.K:
-            raise ValueError("state_dict level_index outside the current pool of %d levels"
-                             % self.pool.K)
+            import warnings
+            warnings.warn("state_dict level_index outside the current pool of %d levels"
+                          " (informational only)" % self.pool.K)
         self.board.copy_(d["board"])
         self.goals.copy_(d["goals"])
         self.start_board.copy_(d["start_board"])

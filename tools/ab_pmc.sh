@@ -13,7 +13,7 @@ for spec in "$@"; do
 import json, sys
 d = json.load(open(sys.argv[1]))
 for k, v in d["kernels"].items():
-    if "k_env_step" in k or "prologue" in k or "k_env_action" in k:
+    if "k_env_step" in k or "prologue" in k or "draw" in k or "k_env_action" in k:
         g = lambda key: v.get(key) or v.get("last_" + key) or 0
         print(sys.argv[2], k[:48], "us=%.1f" % (g("avg_ns") / 1e3),
               "valu/w=%.0f salu/w=%.0f" % (v.get("valu_per_wave", 0), v.get("salu_per_wave", 0)),
