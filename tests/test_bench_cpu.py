@@ -46,7 +46,12 @@ def test_labels():
     assert bench.step_kernel_name(25, 40, "none", "auto") == "k_env_step_small<0>"
     assert bench.step_kernel_name(128, 128, "none", "auto") == "k_env_step_bits128<0>"
     assert (bench.step_kernel_name(128, 128, "none", "auto", "stream")
-            == "k_env_step_bits128<1>")
+            == "k_env_step_bits128<3>")                  # draws decided before the step
+    assert (bench.step_kernel_name(64, 64, "none", "auto", "stream")
+            == "k_env_step_bits64<false, 1>")
+    # replay without any spawner runs the Philox form
+    assert (bench.step_kernel_name(64, 64, "none", "auto", "stream", replay=False)
+            == "k_env_step_bits64<false, 0>")
     assert bench.step_kernel_name(64, 64, "none", "generic") == "k_env_step_generic"
 
 
@@ -58,6 +63,9 @@ def test_pmc_record_keyed_on_build(tmp_path, monkeypatch):
     (prof / "pmc_c3.json").write_text(json.dumps(rec))
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
     assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits64<false, 0>")[0] == 123.0
+    # replay lines keep their own record
+    assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits64<false, 0>",
+                                     "stream")[0] is None
     assert bench.traffic_from_record("c3", "none", "other", "k_env_step_bits64<false, 0>")[0] is None
     assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits128<0>")[0] is None
     assert bench.traffic_from_record("c5", "none", "abc", "k_env_step_bits128<0>")[0] is None
