@@ -436,11 +436,9 @@ k_env_step_bits128(Step128KArgs ka) {
 // on the bit-sliced rule.  When the last step was a decided replay step (planes_ok
 // bit 3) the board's eligible cells are already in its draw planes, bar the rows the
 // action edited: 2 KiB per env and a few board rows instead of the 32 KiB board.
-__global__ void __launch_bounds__(64)
-k_stream_prologue128(Step128KArgs ka) {
+__device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, int lane,
+                                            int &nb_out, int &ng_out, int &dfl_out) {
     const sl_env_state &st = ka.st;
-    const int64_t b = blockIdx.x;
-    const int lane = threadIdx.x;
     const int64_t off = b * (int64_t)(N * N);
     const u32 *gb = reinterpret_cast<const u32 *>(st.board + off) + lane;
     const u32 *gg = reinterpret_cast<const u32 *>(st.goals + off) + lane;
@@ -548,13 +546,23 @@ k_stream_prologue128(Step128KArgs ka) {
         if (nb < 0) nb = count(gb, 0);
     }
     const int ng = ((rec(V, R_POK) & 6) == 6 || !(spf & 2)) ? 0 : count(gg, 1);
+    const int dfl = (nb ? 1 : 0) | (ng ? 2 : 0);
     if (lane == 0) {
         w.counts[2 * b] = nb;
         w.counts[2 * b + 1] = ng;
-        // the tensors that draw, for k_stream_draw128 and the step (the action's edited
-        // rows in this slot have been read)
-        if (dp) w.act[st.B + b] = (nb ? 1 : 0) | (ng ? 2 : 0);
+        // the tensors that draw, for the draws and the step (the action's edited rows
+        // in this slot have been read)
+        if (dp) w.act[st.B + b] = dfl;
     }
+    nb_out = nb;
+    ng_out = ng;
+    dfl_out = dfl;
+}
+
+__global__ void __launch_bounds__(64)
+k_stream_prologue128(Step128KArgs ka) {
+    int nb, ng, dfl;
+    count_env128(ka, blockIdx.x, threadIdx.x, nb, ng, dfl);
 }
 
 // The two 32x32 bit matrices held by lanes 0-31 and 32-63, transposed within each
@@ -605,13 +613,10 @@ __device__ __forceinline__ int scan_halves(int v) {
 // eligible row.
 constexpr int kDrawBatch = 8;
 constexpr int kSegs = NB * 64;
-__global__ void __launch_bounds__(64)
-k_stream_draw128(Step128KArgs ka) {
+__device__ __forceinline__ void draw_env128(const Step128KArgs &ka, int64_t b, int lane, int dfl,
+                                           int64_t pos_b, int64_t pos_g) {
     const sl_env_state &st = ka.st;
-    const int64_t b = blockIdx.x;
-    const int lane = threadIdx.x;
     const Scratch w = scratch_of(ka.fx.scratch, st.B);
-    const int dfl = (int)w.act[st.B + b];
     if (!(dfl & 3)) return;
     __shared__ u32 segb_[kSegs];
     __shared__ u32 segr_[2 * kSegs];   // [segment][word]
@@ -640,7 +645,7 @@ k_stream_draw128(Step128KArgs ka) {
                     dp[(tensor * NB + t) * 128 + 64 * q] = thr >= 1.0 ? E[t][q] : 0u;
             continue;
         }
-        const int64_t pos = w.offsets[2 * b + tensor];
+        const int64_t pos = tensor ? pos_g : pos_b;
         // the segments: bases and cells
         int total = 0;
         const int half = lane >> 5;
@@ -712,6 +717,13 @@ k_stream_draw128(Step128KArgs ka) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // before the next tensor's
         __builtin_amdgcn_wave_barrier();                        // segment writes
     }
+}
+
+__global__ void __launch_bounds__(64)
+k_stream_draw128(Step128KArgs ka) {
+    const int64_t b = blockIdx.x;
+    const Scratch w = scratch_of(ka.fx.scratch, ka.st.B);
+    draw_env128(ka, b, threadIdx.x, (int)w.act[ka.st.B + b], w.offsets[2 * b], w.offsets[2 * b + 1]);
 }
 
 }  // namespace
