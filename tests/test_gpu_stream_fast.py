@@ -182,3 +182,59 @@ def test_small_shapes_stream_vs_generic(torch_dev, shape):
         _compare_state(fast, gen, (shape, t))
     assert fast.stream_pos.item() > 0
     assert not fast.stream_error()
+
+
+@pytest.mark.parametrize("case", ["toggle_powers", "p1", "p0", "wrap_rows"])
+def test_decided_replay128_edges_vs_generic(torch_dev, case):
+    """The 128x128 replay path's own state (sl_env_state.elig_planes: the eligibility
+    the step leaves, patched around the action's rows; the draw pass's decisions)
+    against the per-cell replay, which keeps none of it, on the cases that path
+    special-cases: actions that create and destroy spawners (can_toggle_powers: the
+    spawn flags are forced and the patch window must see new spawners), spawn
+    probability 1 and 0 (draws consumed, never compared), and agents on the rows
+    around the 127/0 wrap (the patch window straddles it)."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    pool = _sprinkled(C5_POOL, 5, 0.0)
+    al = np.stack([pool.agent_x, pool.agent_y], 1)
+    sp = pool.spawn_prob.copy()
+    if case == "p1":
+        sp[:] = 1.0
+    elif case == "p0":
+        sp[:] = 0.0
+    if case == "wrap_rows":        # levels rolled so the agents start on rows 126, 127, 0, 1
+        board, goals = pool.board.copy(), pool.goals.copy()
+        for k in range(pool.K):
+            sh = (126 + k - int(pool.agent_y[k])) % 128
+            board[k] = np.roll(pool.board[k], sh, 0)
+            goals[k] = np.roll(pool.goals[k], sh, 0)
+            al[k, 1] = (int(pool.agent_y[k]) + sh) % 128
+        pool = LevelPool(board, goals, al, pool.orientation, sp, pool.min_performance)
+    else:
+        pool = LevelPool(pool.board, pool.goals, al, pool.orientation, sp, pool.min_performance)
+    B, T = 48, 40
+    stream = np.random.RandomState(29).random_sample(60_000_000)
+    kw = dict(time_limit=25, view_shape=(15, 15), output_channels=None, penalty_coef=1.0,
+              min_performance=0.01, rng="stream", spawn_stream=stream, level_order="random",
+              augment_roll=(case != "wrap_rows"),
+              can_toggle_powers=(case == "toggle_powers"),
+              can_toggle_colors=(case == "toggle_powers"))
+    fast = SafeLifeVecEnv(pool, B, "cuda:0", kernel="fast", **kw)
+    gen = SafeLifeVecEnv(pool, B, "cuda:0", kernel="generic", **kw)
+    assert fast.elig_planes is not None
+    assert torch.equal(fast.reset(), gen.reset())
+    rng = np.random.RandomState(8)
+    moves = 0
+    for t in range(T):
+        a = torch.from_numpy(rng.choice(9, size=B, p=[.04] + [.12] * 4 + [.12] * 4)
+                             .astype(np.int32)).to(dev)
+        o1, r1, d1, _ = fast.step(a)
+        o2, r2, d2, _ = gen.step(a)
+        assert torch.equal(r1, r2), (case, t)
+        assert torch.equal(d1, d2), (case, t)
+        assert torch.equal(o1, o2), (case, t)
+        assert fast.stream_pos.item() == gen.stream_pos.item(), (case, t)
+        _compare_state(fast, gen, (case, t))
+        moves += int((a > 0).sum().item())
+    assert moves > 0 and fast.stream_pos.item() > 0
+    assert not fast.stream_error()
