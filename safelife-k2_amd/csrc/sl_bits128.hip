@@ -26,8 +26,14 @@
 //    their three colour planes are read, per band, for the scores;
 //  * the action (execute_action / move_agent, safelife_game.py:308-393) has run
 //    before this kernel: k_env_action (one lane per env, both RNG modes) leaves the
-//    state and cell edits in HBM and the reward in the scratch (in replay mode
-//    k_stream_prologue128 then counts the draws);
+//    state and cell edits in HBM and the reward in the scratch;
+//  * replay mode (SL_RNG_STREAM, the reference's stream order) with draw planes
+//    (sl_env_state.elig_planes): k_stream_prologue128 counts each tensor's eligible
+//    cells -- for the board from the eligibility the last step left, patched around
+//    the action's rows -- sl_exclusive_scan_i64 places them in the stream,
+//    k_stream_draw128 decides every spawn, and this kernel (SPAWN_DECIDED) ANDs the
+//    decisions into its spawns and leaves the advanced board's eligibility for the
+//    next step's count;
 //  * exits are rewritten by the epilogue after the band stores have completed.
 // Finished envs are queued and reset by a follow-up kernel (k_env_reset_list_wide,
 // one 1024-thread block per env).
