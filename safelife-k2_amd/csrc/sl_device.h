@@ -28,11 +28,14 @@ __device__ __forceinline__ void philox4x32(uint32_t c0, uint32_t c1, uint32_t c2
                                            uint64_t seed, uint32_t out[4]) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     // two rounds per iteration (no register rotation moves); fully unrolled inside the
-    // bit-sliced kernels' draw loops it cost the 64x64 kernel 64 spilled VGPRs
+    // bit-sliced kernels' draw loops it cost the 64x64 kernel 64 spilled VGPRs.  Each
+    // product is one v_mad_u64_u32 (hi and lo together; a v_mul_hi_u32 + v_mul_lo_u32
+    // pair before: C5 1.169 -> 1.165 ms, tools/ab/c5_philox_mad.py)
 #pragma unroll 2
     for (int r = 0; r < 10; r++) {
-        uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         uint32_t n0 = hi1 ^ c1 ^ k0;
         uint32_t n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
