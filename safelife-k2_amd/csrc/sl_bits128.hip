@@ -185,7 +185,7 @@ __device__ __forceinline__ u32 pack_row(const u32 pl[8], int y) {
 // neighbouring rows up / dn (row dwords); the rest of the rule folds away.  Stored as
 // the board's draw planes, which k_stream_prologue128 patches and counts.
 __device__ __forceinline__ void next_elig(const u32 pl[8], u32 up, u32 dn, int t, int lane,
-                                          u32 *me) {
+                                          u32 *me, uint16_t *cnt) {
     u32 P[32];
 #pragma unroll
     for (int k = 0; k < 32; k++) P[k] = 0u;
@@ -200,6 +200,8 @@ __device__ __forceinline__ void next_elig(const u32 pl[8], u32 up, u32 dn, int t
     rule_planes(P, ch, geo, sc, 0u);
     __builtin_nontemporal_store(geo.e[0], &me[kDrawPlanes + t * 128]);
     __builtin_nontemporal_store(geo.e[1], &me[kDrawPlanes + t * 128 + 64]);
+    const int n = wave_total(__builtin_popcount(geo.e[0]) + __builtin_popcount(geo.e[1]));
+    if (lane == 0) cnt[t] = (uint16_t)n;       // the band's count (<= 4096)
 }
 
 // all kernel arguments in one struct at kernarg offset 0: the epilogue re-reads its
@@ -341,6 +343,10 @@ k_env_step_bits128(Step128KArgs ka) {
     // has advanced, bands 3 and 0 after the loop
     __attribute__((address_space(3))) u32 *e0 = (__attribute__((address_space(3))) u32 *)slots_;
     u32 EP[8], r31 = 0u, d1 = 0u;
+    // and their count per band, for the next step's count (scratch act[2B + b], four
+    // 16-bit band counts)
+    uint16_t *ne_cnt = MODE == SPAWN_DECIDED ? reinterpret_cast<uint16_t *>(w.act + 2 * st.B + b)
+                                             : nullptr;
 #pragma unroll 1
     for (int t = 0; t < NB; t++) {
         u32 P[32];
@@ -365,7 +371,7 @@ k_env_step_bits128(Step128KArgs ka) {
             for (int s = 0; s < 4; s++)
 #pragma unroll
                 for (int q = 0; q < 2; q++) EC[2 * s + q] = PL(P, elig_plane(s), q);
-            if (t >= 2) next_elig(EP, r31, pack_row(EC, 0), t - 1, lane, me);
+            if (t >= 2) next_elig(EP, r31, pack_row(EC, 0), t - 1, lane, me, ne_cnt);
             if (t == 1) d1 = pack_row(EC, 0);
             if (t >= 1) r31 = pack_row(EP, 31);
 #pragma unroll
@@ -411,8 +417,8 @@ k_env_step_bits128(Step128KArgs ka) {
         u32 E0[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) E0[k] = e0[k * 64 + lane];
-        next_elig(EP, r31, pack_row(E0, 0), NB - 1, lane, me);
-        next_elig(E0, pack_row(EP, 31), d1, 0, lane, me);
+        next_elig(EP, r31, pack_row(E0, 0), NB - 1, lane, me, ne_cnt);
+        next_elig(E0, pack_row(EP, 31), d1, 0, lane, me, ne_cnt);
     }
     const int points = wave_total(pts), score = wave_total(scr);
     const int possible = wave_total(pos), side_total = wave_total(side);
@@ -486,11 +492,10 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
     // rows y - 1 .. y + 1 of each edited row y.  Returns -1 when the edited rows do not
     // fit one window (the full count then runs).
     auto count_next = [&]() -> int {
-        u32 E[NB][2];
-#pragma unroll
-        for (int t = 0; t < NB; t++)
-#pragma unroll
-            for (int q = 0; q < 2; q++) E[t][q] = dp[t * 128 + 64 * q];
+        // their count, as the step left it (scratch act[2B + b]: four 16-bit band counts)
+        const uint64_t nc = (uint64_t)w.act[2 * st.B + b];
+        const int n0 = (int)((nc & 0xFFFFu) + ((nc >> 16) & 0xFFFFu) + ((nc >> 32) & 0xFFFFu) +
+                             (nc >> 48));
         const u32 rows = (u32)w.act[st.B + b];
         int y0 = -1, dmin = 0, dmax = 0;
 #pragma unroll
@@ -502,45 +507,43 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
             dmin = min(dmin, d);
             dmax = max(dmax, d);
         }
-        if (y0 >= 0) {
-            if (dmax - dmin > 27) return -1;
-            const int base = (y0 + dmin - 2) & (N - 1), nrows = dmax - dmin + 5;
-            u32 P[32];
+        if (y0 < 0) return n0;                          // nothing edited: as the step left it
+        if (dmax - dmin > 27) return -1;
+        const int base = (y0 + dmin - 2) & (N - 1), nrows = dmax - dmin + 5;
+        u32 P[32];
 #pragma unroll
-            for (int i = 0; i < 32; i++) P[i] = i < nrows ? gb[((base + i) & (N - 1)) * RS] : 0u;
-            transpose32(P);
+        for (int i = 0; i < 32; i++) P[i] = i < nrows ? gb[((base + i) & (N - 1)) * RS] : 0u;
+        transpose32(P);
 #pragma unroll
-            for (int k = 0; k < 16; k++)
-                if (k != 0 && k != 4 && k != 6 && k != 7) PL(P, k, 0) = PL(P, k, 1) = 0u;
-            GeoBand<SPAWN_COUNT> geo{lane, 0, HaloView{0u, 0u}, none, 0, 0, 0, nullptr};
-            u32 ch[2];
-            rule_planes(P, ch, geo, sc, 0u);
-            u32 rm = 0u;                                // window rows re-evaluated
+        for (int k = 0; k < 16; k++)
+            if (k != 0 && k != 4 && k != 6 && k != 7) PL(P, k, 0) = PL(P, k, 1) = 0u;
+        GeoBand<SPAWN_COUNT> geo{lane, 0, HaloView{0u, 0u}, none, 0, 0, 0, nullptr};
+        u32 ch[2];
+        rule_planes(P, ch, geo, sc, 0u);
+        u32 rm = 0u;                                    // window rows re-evaluated
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int y = (int)((rows >> (8 * j)) & 0xFFu);
-                if (y < N) rm |= 7u << (((y - base) & (N - 1)) - 1);
-            }
-            const int sh = base & 31, tb = base >> 5;
-#pragma unroll
-            for (int t = 0; t < NB; t++)
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    if (t == tb)
-                        E[t][q] = (E[t][q] & ~(rm << sh)) | ((geo.e[q] & rm) << sh);
-                    if (sh && t == ((tb + 1) & (NB - 1)))
-                        E[t][q] = (E[t][q] & ~(rm >> (32 - sh))) | ((geo.e[q] & rm) >> (32 - sh));
-                }
+        for (int j = 0; j < 4; j++) {
+            const int y = (int)((rows >> (8 * j)) & 0xFFu);
+            if (y < N) rm |= 7u << (((y - base) & (N - 1)) - 1);
         }
-        int n = 0;
+        // the window spans band tb from bit sh on and, when sh > 0, the start of the
+        // next band: only those words are read, patched and written back
+        const int sh = base & 31, tb = base >> 5, tn = (tb + 1) & (NB - 1);
+        int dn = 0;                                     // eligible cells gained - lost
 #pragma unroll
-        for (int t = 0; t < NB; t++)
-#pragma unroll
-            for (int q = 0; q < 2; q++) {
-                n += __builtin_popcount(E[t][q]);
-                dp[t * 128 + 64 * q] = E[t][q];
+        for (int q = 0; q < 2; q++) {
+            const u32 ma = rm << sh, na = (geo.e[q] & rm) << sh;
+            const u32 a = dp[tb * 128 + 64 * q];
+            dn += __builtin_popcount(na) - __builtin_popcount(a & ma);
+            dp[tb * 128 + 64 * q] = (a & ~ma) | na;
+            if (sh) {
+                const u32 mc = rm >> (32 - sh), nc = (geo.e[q] & rm) >> (32 - sh);
+                const u32 c = dp[tn * 128 + 64 * q];
+                dn += __builtin_popcount(nc) - __builtin_popcount(c & mc);
+                dp[tn * 128 + 64 * q] = (c & ~mc) | nc;
             }
-        return wave_total(n);
+        }
+        return n0 + wave_total(dn);
     };
     // a board or goals without spawners (spawn_flags, set at reset: no rule or action
     // creates one) draws nothing; nor do goals at their fixed point (planes_ok bit 2)

@@ -13,7 +13,8 @@ namespace sl {
 //   [4B, 8B)  per env: action reward, d_points, d_score, d_side of the action's
 //             cell edits (the generic path; the bit-sliced replay prologues write
 //             the reward only; 128x128 replay with elig_planes: [B, 2B) holds the
-//             rows the action edited, then the tensors that draw, bit0 board, bit1 goals)
+//             rows the action edited, then the tensors that draw, bit0 board, bit1 goals;
+//             [2B, 3B) the count of the board eligibility the step left)
 //   [8B]      error flags (bit0: draw stream exhausted)
 //   [8B+2], [8B+3]  reset-list lengths for even / odd steps (each step's reset
 //             kernel zeroes the other one)
