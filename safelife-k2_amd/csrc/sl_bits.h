@@ -131,6 +131,15 @@ __device__ __forceinline__ u32 wave_or(u32 v) {
            (u32)__builtin_amdgcn_readlane((int)v, 32) | (u32)__builtin_amdgcn_readlane((int)v, 48);
 }
 
+// this lane's index, recomputed where it is used (v_mbcnt): the asm keeps the compiler
+// from hoisting it, and every address derived from it, out of a loop and holding them
+// (or spilling them) through it; two VALU per use against a register held throughout
+__device__ __forceinline__ int lane_now() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -139,7 +148,15 @@ struct SpawnCtx {
     uint32_t gid, step;
     uint64_t seed;
     double thr;
+    uint32_t lim;      // Philox compare limit, ceil(thr * 2^32) - 1 (set_spawn_prob)
 };
+// thr = (double)(float)p, the reference's compare (advance_board.c:109-113), and its
+// integer form for 32-bit Philox words: word * 2^-32 < thr  <=>  word <= lim (0 < thr <
+// 1; both exact).  Computed once per env, wave-uniform, so the draws hold no double.
+__device__ __forceinline__ void set_spawn_prob(SpawnCtx &sc, float p) {
+    sc.thr = (double)p;
+    sc.lim = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ceil(sc.thr * 4294967296.0) - 1.0));
+}
 
 // How a geometry draws the spawns of its eligible cells (Geo::spawn):
 //   SPAWN_PHILOX  Philox keyed by (cell, env, step, tensor): no ordering needed;
@@ -166,8 +183,7 @@ struct StreamSrc {
 template <class Geo>
 __device__ __forceinline__ void lane_draws(const Geo &g, const u32 elig[2], u32 sp[2],
                                            const SpawnCtx &sc, u32 tensor) {
-    // word * 2^-32 < thr  <=>  word <= ceil(thr * 2^32) - 1 (0 < thr < 1; both exact)
-    const u32 lim = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(ceil(sc.thr * 4294967296.0) - 1.0));
+    const u32 lim = sc.lim;
     const u32 any = elig[0] | elig[1];
     u32 blocks = (any | (any >> 1)) & 0x55555555u, s0 = 0u, s1 = 0u;
     while (blocks) {
@@ -214,7 +230,7 @@ constexpr int kDrawSlots = 1024;
 template <class Geo>
 __device__ __forceinline__ void compact_draws(const Geo &g, const u32 elig[2], u32 sp[2],
                                               const SpawnCtx &sc, u32 tensor, lds_u16 *slots) {
-    const u32 lim = (u32)__builtin_amdgcn_readfirstlane((int)(u32)(ceil(sc.thr * 4294967296.0) - 1.0));
+    const u32 lim = sc.lim;
     const u32 any = elig[0] | elig[1];
     const u32 blocks = (any | (any >> 1)) & 0x55555555u;
     const int cnt = __builtin_popcount(blocks);

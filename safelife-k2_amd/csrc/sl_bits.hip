@@ -472,7 +472,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     sc.gid = a.env0 + (uint32_t)b;
     sc.step = a.step;
     sc.seed = a.seed;
-    sc.thr = (double)__int_as_float(rec(V, R_SPAWN));
+    set_spawn_prob(sc, __int_as_float(rec(V, R_SPAWN)));
     StreamSrc ssrc{a.draws, a.n_draws, nullptr};
     int64_t pos_b = 0, pos_g = 0;
     if (MODE == SPAWN_STREAM) {

@@ -50,12 +50,26 @@ namespace {
 // transpose (43.9 vs 38.6 M env-steps/s) and beat gathering the planes from L2 into
 // registers held across the rule (32.9 vs 37.1); prefetching the next band a band
 // ahead gave nothing (the start-board loads queue behind it, vmcnt is in order).
-constexpr int kMinWaves = 2;  // waves per SIMD the register budget is sized for
+// waves per SIMD the register budget is sized for: 4 (<= 128 VGPRs, with 10 KiB of LDS
+// per wave) for the Philox and decided-replay forms; the stream form (replay without
+// draw planes, a fallback) keeps its in-kernel ranks and stream loads at 3
+constexpr int kMinWaves = 4;
+constexpr int kMinWavesStream = 3;
 
 constexpr int N = 128;       // rows = columns
 constexpr int RS = N / 2;    // dwords per row
 constexpr int NB = N / 32;   // bands of 32 rows
 constexpr int MW = 32 * 64;  // mirror dwords per band (32 words x 64 lanes)
+
+// A per-lane view of a per-env array (element i of lane l at base[i + l]): the base
+// stays wave-uniform (SGPRs) and each access adds a 32-bit lane offset (lane_now), so
+// the kernel holds no per-lane pointers through its bands.
+template <class T>
+struct LanePtr {
+    T *base;
+    __device__ __forceinline__ T &operator[](int i) const { return base[(uint32_t)(i + lane_now())]; }
+    __device__ __forceinline__ T *operator+(int i) const { return base + (uint32_t)(i + lane_now()); }
+};
 
 // The rows just outside a band as "planes": element p is a word with bit 31 = bit p
 // of the row above's cell pair and bit 0 = bit p of the row below's, computed where
@@ -115,16 +129,26 @@ struct GeoBand {
     }
 };
 
-// The start-board planes the side-effect term reads (0, 2, 7-15), from the level
-// pool's bit planes when the env was reset from the pool: row y of
+// The start-board planes the side-effect term reads (0, 2, 7-11, 15; 12-14 below),
+// from the level pool's bit planes when the env was reset from the pool: row y of
 // band t is level row 32t + y - dy, one funnel shift of two adjacent 32-row words;
 // column c is level column c - dx.  At a band's
 // start one global_load_lds per plane copies the two level bands it spans (lanes
-// 0-31: band q0, lanes 32-63: band q1, 128 columns each) into the wave's 11 KiB
+// 0-31: band q0, lanes 32-63: band q1, 128 columns each) into the wave's 8 KiB
 // buffer, so the copy runs under the band's rule and holds no registers; after the
-// rule each word is two LDS reads and a funnel shift.
-constexpr int kPoolPlanes = 11;      // planes 0, 2, 7-15
-__device__ __forceinline__ int pool_plane(int s) { return s == 0 ? 0 : (s == 1 ? 2 : s + 5); }
+// rule each word is two LDS reads and a funnel shift.  A start board written by the
+// caller (start_roll = -1) is loaded from HBM at the band's start and its planes are
+// put into the same buffer (as an unrolled level: dy = dx = 0).
+// Cell bits 12-14 are used by no cell type, so the spool leaves their planes out
+// (8 KiB + 2 KiB of draw slots: 4 waves/SIMD).  The side-effect term then compares the
+// board's planes 12-14 against 0; an env whose start board may carry those bits
+// (spawn_flags bit 2, set where a start board is written: the resets, from the level;
+// the host, for boards it loads) gets the exact term from a second pass over the band
+// (side_hi_fix).
+constexpr int kPoolPlanes = 8;       // planes 0, 2, 7-11, 15
+__device__ __forceinline__ int pool_plane(int s) {
+    return s == 0 ? 0 : (s == 1 ? 2 : (s < 7 ? s + 5 : 15));
+}
 
 __device__ __forceinline__ void pool_dma128(const u32 *__restrict__ pp, int t, int dy, int lane,
                                             __attribute__((address_space(3))) u32 *buf) {
@@ -137,6 +161,47 @@ __device__ __forceinline__ void pool_dma128(const u32 *__restrict__ pp, int t, i
                                          (__attribute__((address_space(3))) void *)(buf + s * 256),
                                          16, 0, 0);
     }
+}
+
+// a start band loaded by the caller's rows (start_roll = -1) into the spool, in
+// pool_start_lds' layout with dy = dx = 0 (word w of lane j at column 2j + w)
+__device__ __forceinline__ void start_band_lds(const u32 *__restrict__ src, int lane,
+                                               __attribute__((address_space(3))) u32 *buf) {
+    u32 S[32];
+    load_pairs<RS>(src, S);
+    transpose32(S);
+#pragma unroll
+    for (int s = 0; s < kPoolPlanes; s++) {
+        buf[s * 256 + 2 * lane] = PL(S, pool_plane(s), 0);
+        buf[s * 256 + 2 * lane + 1] = PL(S, pool_plane(s), 1);
+    }
+}
+
+// The band's side-effect count with the start board's planes 12-14 taken into account
+// (score_planes counted them as 0): B the band's advanced planes, S its start planes
+// as read from the spool (12-14 zero), src the start band's rows in HBM.  Returns the
+// correction to add.  Only for envs whose start board may use cell bits 12-14.
+__device__ __forceinline__ int side_hi_fix(const u32 B[32], const u32 gc[3][2], u32 S[32],
+                                           const u32 *__restrict__ src) {
+    int e0, e1, x;
+    score_planes(B, gc, S, &x, &x, &x, &e0);
+    u32 h[3][2] = {{0u, 0u}, {0u, 0u}, {0u, 0u}};
+#pragma unroll 1
+    for (int y = 0; y < 32; y++) {
+        const u32 d = src[y * RS];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            h[k][0] |= ((d >> (12 + k)) & 1u) << y;
+            h[k][1] |= ((d >> (28 + k)) & 1u) << y;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        PL(S, 12 + k, 0) = h[k][0];
+        PL(S, 12 + k, 1) = h[k][1];
+    }
+    score_planes(B, gc, S, &x, &x, &x, &e1);
+    return e1 - e0;
 }
 
 __device__ __forceinline__ void pool_start_lds(const __attribute__((address_space(3))) u32 *buf,
@@ -159,11 +224,11 @@ __device__ __forceinline__ void pool_start_lds(const __attribute__((address_spac
 // the decided spawns of band t of a tensor (0 board, 1 goals) for the step kernel's
 // rule: loaded at the band's start, under its row loads; none when the tensor draws
 // nothing this step (`draws` false)
-template <class G>
-__device__ __forceinline__ void draw_planes(G &geo, const u32 *me, int tensor, int t, bool draws) {
+template <class G, class M>
+__device__ __forceinline__ void draw_planes(G &geo, const M &me, int tensor, int t, bool draws) {
     geo.e[0] = geo.e[1] = 0u;
     if (draws) {
-        const u32 *d = me + kDrawPlanes + (tensor * NB + t) * 128;
+        const u32 *d = me + (kDrawPlanes + (tensor * NB + t) * 128);
         geo.e[0] = d[0];
         geo.e[1] = d[64];
     }
@@ -184,8 +249,9 @@ __device__ __forceinline__ u32 pack_row(const u32 pl[8], int y) {
 // eligibility before its action -- from the band's planes 0, 4, 6, 7 and the
 // neighbouring rows up / dn (row dwords); the rest of the rule folds away.  Stored as
 // the board's draw planes, which k_stream_prologue128 patches and counts.
+template <class M>
 __device__ __forceinline__ void next_elig(const u32 pl[8], u32 up, u32 dn, int t, int lane,
-                                          u32 *me, uint16_t *cnt) {
+                                          const M &me, uint16_t *cnt) {
     u32 P[32];
 #pragma unroll
     for (int k = 0; k < 32; k++) P[k] = 0u;
@@ -229,7 +295,7 @@ __device__ __forceinline__ const Step128KArgs &kargs128() {
 // scratch offsets); or SPAWN_DECIDED (the spawns from the draw planes k_stream_draw128
 // left, replay with sl_env_state.elig_planes).
 template <int MODE>
-__global__ void __launch_bounds__(64, kMinWaves)
+__global__ void __launch_bounds__(64, MODE == SPAWN_STREAM ? kMinWavesStream : kMinWaves)
 k_env_step_bits128(Step128KArgs ka) {
     const sl_env_state &st = ka.st;
     const StepArgs &a = ka.a;
@@ -237,10 +303,10 @@ k_env_step_bits128(Step128KArgs ka) {
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x;
     const int64_t off = b * (int64_t)(N * N);
-    u32 *gb = reinterpret_cast<u32 *>(st.board + off) + lane;      // row r: gb[r * RS]
-    u32 *gg = reinterpret_cast<u32 *>(st.goals + off) + lane;
-    const u32 *gs = reinterpret_cast<const u32 *>(st.start_board + off) + lane;
-    u32 *mg = st.planes + b * (int64_t)(NB * MW) + lane;            // mirror [t][q][lane]
+    const LanePtr<u32> gb{reinterpret_cast<u32 *>(st.board + off)};   // row r: gb[r * RS]
+    const LanePtr<u32> gg{reinterpret_cast<u32 *>(st.goals + off)};
+    const LanePtr<const u32> gs{reinterpret_cast<const u32 *>(st.start_board + off)};
+    const LanePtr<u32> mg{st.planes + b * (int64_t)(NB * MW)};       // mirror [t][q][lane]
 
     const u32 V = load_record(st, ka.actions, b, lane);
     __shared__ __attribute__((aligned(16))) u32 spool_[kPoolPlanes * 256];
@@ -253,14 +319,14 @@ k_env_step_bits128(Step128KArgs ka) {
     // replay with draw planes: the spawns come decided from them (k_stream_draw128), for
     // the tensors that draw (scratch act[B + b] bit 0 board, bit 1 goals), and the
     // advanced board's eligible cells go back into the board's planes
-    u32 *me = MODE == SPAWN_DECIDED ? st.elig_planes + b * kEligStride + lane : nullptr;
+    const LanePtr<u32> me{MODE == SPAWN_DECIDED ? st.elig_planes + b * kEligStride : nullptr};
     const int dfl = MODE == SPAWN_DECIDED ? (int)w.act[st.B + b] : 0;
 
     SpawnCtx sc;
     sc.gid = a.env0 + (uint32_t)b;
     sc.step = a.step;
     sc.seed = a.seed;
-    sc.thr = (double)__int_as_float(rec(V, R_SPAWN));
+    set_spawn_prob(sc, __int_as_float(rec(V, R_SPAWN)));
     StreamSrc ssrc{a.draws, a.n_draws, nullptr};
     int64_t pos_b = 0, pos_g = 0;
     if (MODE == SPAWN_STREAM) {
@@ -288,7 +354,7 @@ k_env_step_bits128(Step128KArgs ka) {
             const u32 last = G[31];
             transpose32(G);
             u32 cg[2];
-            GeoBand<MODE> geo{lane, 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_g, 0, 0, slots};
+            GeoBand<MODE> geo{lane_now(), 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_g, 0, 0, slots};
             if (MODE == SPAWN_DECIDED) draw_planes(geo, me, 1, t, dfl & 2);
             rule_planes(G, cg, geo, sc, 1u);
             pos_g += geo.used;
@@ -317,12 +383,6 @@ k_env_step_bits128(Step128KArgs ka) {
     }
     __builtin_amdgcn_sched_barrier(0);
 
-    const int act_reward = (int)w.act[b];
-    RecFields fl{V, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), 0.0};
-    if (a.bonus_period > 0)        // issued now, consumed by the epilogue
-        fl.bval = a.bonus_table[bonus_dist(fl.ax, fl.ay, fl.prior_x(fl.prior_head()),
-                                           fl.prior_y(fl.prior_head()), fl.prior_len(),
-                                           a.bonus_period, a.bonus_len)];
 
     // ---- board, band by band: rule, scores, changed rows back.  The start board
     // comes from the level pool's planes when the env was reset from it
@@ -333,8 +393,8 @@ k_env_step_bits128(Step128KArgs ka) {
                       st.start_roll) ? rec(V, R_ROLL) : -1;
     const u32 *pp = reinterpret_cast<const u32 *>(pool.board_planes) +
                     (int64_t)(roll >= 0 ? rec(V, R_LI) : 0) * (16 * NB * N);
-    const int sdy = roll >> 16, sdx = roll & 0xFFFF;
-    const int sc0 = (2 * lane - sdx) & (N - 1), sc1 = (sc0 + 1) & (N - 1);
+    const int sdy = roll < 0 ? 0 : roll >> 16, sdx = roll < 0 ? 0 : roll & 0xFFFF;
+    const bool start_hi = (rec(V, R_SPF) & 4) != 0;     // start board may use bits 12-14
     int pts = 0, scr = 0, pos = 0, side = 0;
     u32 up = gb[(N - 1) * RS], row0 = 0;
     // SPAWN_DECIDED: the eligibility planes of the previous band (of band 0 in LDS, in
@@ -352,15 +412,14 @@ k_env_step_bits128(Step128KArgs ka) {
         u32 P[32];
         load_pairs_nt<RS>(gb + 32 * t * RS, P);
         const u32 dn = t < NB - 1 ? gb[(32 * t + 32) * RS] : row0;
-        if (roll >= 0) {
-            wait_lgkm();        // the previous band's reads of the buffer are done
-            pool_dma128(pp, t, sdy, lane, spool);
-        }
+        wait_lgkm();            // the previous band's reads of the buffer are done
+        if (roll >= 0) pool_dma128(pp, t, sdy, lane_now(), spool);
+        else start_band_lds(gs + 32 * t * RS, lane_now(), spool);
         if (t == 0) row0 = P[0];
         const u32 last = P[31];
         transpose32(P);
         u32 cb[2];
-        GeoBand<MODE> geo{lane, 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_b, 0, 0, slots};
+        GeoBand<MODE> geo{lane_now(), 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_b, 0, 0, slots};
         if (MODE == SPAWN_DECIDED) draw_planes(geo, me, 0, t, dfl & 1);
         rule_planes(P, cb, geo, sc, 0u);
         pos_b += geo.used;
@@ -371,12 +430,12 @@ k_env_step_bits128(Step128KArgs ka) {
             for (int s = 0; s < 4; s++)
 #pragma unroll
                 for (int q = 0; q < 2; q++) EC[2 * s + q] = PL(P, elig_plane(s), q);
-            if (t >= 2) next_elig(EP, r31, pack_row(EC, 0), t - 1, lane, me, ne_cnt);
+            if (t >= 2) next_elig(EP, r31, pack_row(EC, 0), t - 1, lane_now(), me, ne_cnt);
             if (t == 1) d1 = pack_row(EC, 0);
             if (t >= 1) r31 = pack_row(EP, 31);
 #pragma unroll
             for (int k = 0; k < 8; k++) {
-                if (t == 0) e0[k * 64 + lane] = EC[k];
+                if (t == 0) e0[k * 64 + lane_now()] = EC[k];
                 EP[k] = EC[k];
             }
         }
@@ -390,14 +449,13 @@ k_env_step_bits128(Step128KArgs ka) {
         }
         int p, q, r, e;
         u32 S[32];
-        if (roll < 0) {
-            load_pairs<RS>(gs + 32 * t * RS, S);
-            transpose32(S);
-        } else {
-            wait_vm();          // the band's pool planes have landed in LDS
+        wait_vm();              // the band's start planes have landed in LDS
+        {
+            const int sc0 = (2 * lane_now() - sdx) & (N - 1), sc1 = (sc0 + 1) & (N - 1);
             pool_start_lds(spool, t, sdy, sc0, sc1, S);
         }
         score_planes(P, gcol, S, &p, &q, &r, &e);
+        if (start_hi) e += side_hi_fix(P, gcol, S, gs + 32 * t * RS);
         pts += p;
         scr += q;
         pos += r;
@@ -416,19 +474,28 @@ k_env_step_bits128(Step128KArgs ka) {
     if (MODE == SPAWN_DECIDED) {
         u32 E0[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) E0[k] = e0[k * 64 + lane];
-        next_elig(EP, r31, pack_row(E0, 0), NB - 1, lane, me, ne_cnt);
-        next_elig(E0, pack_row(EP, 31), d1, 0, lane, me, ne_cnt);
+        for (int k = 0; k < 8; k++) E0[k] = e0[k * 64 + lane_now()];
+        next_elig(EP, r31, pack_row(E0, 0), NB - 1, lane_now(), me, ne_cnt);
+        next_elig(E0, pack_row(EP, 31), d1, 0, lane_now(), me, ne_cnt);
     }
     const int points = wave_total(pts), score = wave_total(scr);
     const int possible = wave_total(pos), side_total = wave_total(side);
     // goals mirror bits, and bit 3 = the board's draw planes hold the advanced board's
     // eligible cells (decided replay only: any other step clears it)
-    const int ok = gok | (me ? 8 : 0);
-    if (ok != pok_all && lane == 0) st.planes_ok[b] = ok;
+    const int ok = gok | (me.base ? 8 : 0);
+    if (ok != pok_all && lane_now() == 0) st.planes_ok[b] = ok;
+    // the epilogue's inputs, loaded now (in flight with the row stores) rather than held
+    // through the bands: the reward, the bonus term and the record again (L2)
+    const Step128KArgs &k = kargs128();
+    const u32 VE = load_record(k.st, k.actions, b, lane_now());
+    const int act_reward = (int)scratch_of(k.fx.scratch, k.st.B).act[b];
+    RecFields fl{VE, rec(VE, R_GO), rec(VE, R_AX), rec(VE, R_AY), 0.0};
+    if (k.a.bonus_period > 0)
+        fl.bval = k.a.bonus_table[bonus_dist(fl.ax, fl.ay, fl.prior_x(fl.prior_head()),
+                                             fl.prior_y(fl.prior_head()), fl.prior_len(),
+                                             k.a.bonus_period, k.a.bonus_len)];
     wait_vm();              // row stores land before the epilogue rewrites the exits
-    if (lane == 0) {
-        const Step128KArgs &k = kargs128();
+    if (lane_now() == 0) {
         const bool reset = epilogue_core(k.st, k.a, b, fl, act_reward, points, score, possible,
                                          side_total, k.reward_out, k.done_out, k.flags_out,
                                          k.ep_len_out, k.ep_rew_out);

@@ -314,7 +314,7 @@ k_env_step_small(SmallKArgs ka) {
     sc.gid = a.env0 + (uint32_t)b;
     sc.step = a.step;
     sc.seed = a.seed;
-    sc.thr = (double)__int_as_float(rec(V, R_SPAWN));
+    set_spawn_prob(sc, __int_as_float(rec(V, R_SPAWN)));
 
     // ---- goals: rule, then store the changed rows
     transpose32(PG);
@@ -485,7 +485,7 @@ __device__ __forceinline__ void seg_philox(const Geo &g, const u32 elig[2], u32 
         sp[0] = elig[0];
         sp[1] = elig[1];
     } else if (sc.thr > 0.0) {
-        const u32 lim = (u32)(ceil(sc.thr * 4294967296.0) - 1.0);
+        const u32 lim = sc.lim;
         const u32 any = elig[0] | elig[1];
         u32 blocks = (any | (any >> 1)) & 0x55555555u, s0 = 0u, s1 = 0u;
         while (blocks) {
@@ -744,7 +744,7 @@ k_env_step_seg4(SmallKArgs ka) {
     sc.gid = a.env0 + (uint32_t)b;
     sc.step = a.step;
     sc.seed = a.seed;
-    sc.thr = (double)__int_as_float(rc.get(R_SPAWN));
+    set_spawn_prob(sc, __int_as_float(rc.get(R_SPAWN)));
 
     // ---- goals: rule, then store the changed rows
     transpose32(PG);

@@ -20,6 +20,9 @@ constexpr uint32_t LEVEL_EXIT = FROZEN | EXIT;                               // 
 constexpr uint32_t LIFE = ALIVE | DESTR;                                     // 9
 constexpr uint32_t MOVABLE = PUSHABLE | PULLABLE;
 constexpr uint32_t POWERS = ALIVE | INHIBIT | PRESERVE | SPAWN;
+// cell bits no cell type uses (safelife_game.py CellTypes); the 128x128 kernel keeps
+// no start-board planes for them (spawn_flags bit 2 flags a start board that has them)
+constexpr uint32_t kCellHiBits = 0x7000;
 
 // ----------------------------------------------------------------------------
 // Philox4x32-10, counter (c0..c3), key = seed.  Identical to oracle/sl_oracle.c.

@@ -453,6 +453,7 @@ struct ResetShared {
     int wave_tot[NT / 64];
     int exit_y[SL_MAX_EXITS], exit_x[SL_MAX_EXITS];
     int ev, idx, dy, dx;
+    int hi;         // a start-board cell uses bits 12-14 (spawn_flags bit 2)
 };
 
 __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &a,
@@ -466,6 +467,7 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
     if (threadIdx.x == 0) {
         const LevelChoice c = choose_level(pool, a, gid, st.episodes[b], H, W);
         sh_idx = c.idx; sh_dy = c.dy; sh_dx = c.dx;
+        sh.hi = 0;
     }
     __syncthreads();
     const int idx = sh_idx, dy = sh_dy, dx = sh_dx;
@@ -488,6 +490,7 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
             acc[1] += q;
             acc[2] += r;
             acc[3] += ((vb & SPAWN) ? 1 : 0) + ((vg & SPAWN) ? 65536 : 0);  // counts < 2^16
+            if (vb & kCellHiBits) sh.hi = 1;
             ex = (vb & EXIT) != 0;
         }
         int tot;
@@ -500,7 +503,8 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
     }
     block_sum4(acc, red);
     if (threadIdx.x == 0) {
-        const int spawn_bits = ((acc[3] & 0xFFFF) ? 1 : 0) | ((acc[3] >> 16) ? 2 : 0);
+        const int spawn_bits = ((acc[3] & 0xFFFF) ? 1 : 0) | ((acc[3] >> 16) ? 2 : 0) |
+                               (sh.hi ? 4 : 0);
         sh_ev = reset_scalars(st, pool, a, b, idx, dy, dx, acc[0], acc[1], acc[2], spawn_bits);
         st.exit_count[b] = n_exit;
         for (int e = 0; e < SL_MAX_EXITS; e++) {
@@ -532,6 +536,7 @@ struct WideResetShared {
     int red[NTR / 64][4];
     int exl[kExitCap];
     int nex, ev, idx, dy, dx;
+    int hi;         // a start-board cell uses bits 12-14 (spawn_flags bit 2)
 };
 
 __device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &a,
@@ -549,6 +554,7 @@ __device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, co
             sh.dy = c.dy;
             sh.dx = c.dx;
             sh.nex = 0;
+            sh.hi = 0;
         }
     }
     __syncthreads();
@@ -567,6 +573,7 @@ __device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, co
         acc[1] += q;
         acc[2] += r;
         acc[3] += ((vb & SPAWN) ? 1 : 0) + ((vg & SPAWN) ? 65536 : 0);
+        if (vb & kCellHiBits) sh.hi = 1;
         if (vb & EXIT) {
             const int k = atomicAdd(&sh.nex, 1);
             if (k < kExitCap) sh.exl[k] = i;
@@ -581,7 +588,8 @@ __device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, co
         int t[4] = {0, 0, 0, 0};
         for (int w = 0; w < NTR / 64; w++)
             for (int k = 0; k < 4; k++) t[k] += sh.red[w][k];
-        const int spawn_bits = ((t[3] & 0xFFFF) ? 1 : 0) | ((t[3] >> 16) ? 2 : 0);
+        const int spawn_bits = ((t[3] & 0xFFFF) ? 1 : 0) | ((t[3] >> 16) ? 2 : 0) |
+                               (sh.hi ? 4 : 0);
         sh.ev = reset_scalars_from(st, a, b, idx, dy, dx, ls, ep, t[0], t[1], t[2], spawn_bits);
         const int nex = sh.nex;
         int16_t *ey = st.exit_y + b * SL_MAX_EXITS, *ex = st.exit_x + b * SL_MAX_EXITS;

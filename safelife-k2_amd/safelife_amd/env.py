@@ -30,7 +30,7 @@ from . import _lib, speedups
 from .cell_types import CellTypes
 from .levels import LevelPool
 from .spaces import env_spaces
-from .vec_env import ACTION_NAMES, GlobalCounter, SafeLifeVecEnv
+from .vec_env import ACTION_NAMES, GlobalCounter, SafeLifeVecEnv, start_board_hi_bits
 
 # safelife_game.py:27-34
 ORIENTATION = {"UP": 0, "RIGHT": 1, "DOWN": 2, "LEFT": 3, "FORWARD": 4, "BACKWARD": 6}
@@ -424,6 +424,9 @@ class SafeLifeGame:
         else:
             v.start_board[i].copy_(keep_start[0])
             v.state["baseline"][i] = keep_start[1]
+            # spawn_flags bit 2 follows the start board kept (cell bits 12-14)
+            hi = 4 if bool(start_board_hi_bits(v.start_board[i:i + 1])[0]) else 0
+            self._set("spawn_flags", (self._st("spawn_flags") & ~4) | hi)
         # the raw level cells (the reset coloured the exits by can_exit)
         _lib.check(_lib.lib().sl_env_exit_colors(ctypes.byref(self._slice()), 1, self._stream()),
                    "sl_env_exit_colors")

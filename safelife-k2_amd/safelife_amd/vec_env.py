@@ -54,6 +54,12 @@ def _sched(val, counter):
     return val(counter.num_steps) if callable(val) else val
 
 
+def start_board_hi_bits(start_board):
+    """Per env: does any start-board cell use bits 12-14 (used by no cell type)?"""
+    import torch
+    return ((start_board.view(torch.int16) & 0x7000) != 0).flatten(1).any(1)
+
+
 class SafeLifeVecEnv:
     action_names = ACTION_NAMES
 
@@ -484,7 +490,10 @@ class SafeLifeVecEnv:
         longer match pool levels (kernels read them from HBM), the bit-plane
         mirrors are stale and the reset lists start empty."""
         self.st_t["start_roll"].fill_(-1)
-        self.st_t["spawn_flags"].fill_(3)    # may hold spawners: replay counts them
+        # may hold spawners (replay counts them); bit 2: the start board uses cell bits
+        # 12-14, which the 128x128 kernel then compares in a second pass
+        self.st_t["spawn_flags"].copy_(3 | 4 * start_board_hi_bits(self.start_board).to(
+            self.st_t["spawn_flags"].dtype))
         self._may_spawn = True
         self.planes_ok.zero_()
         self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()

@@ -681,6 +681,56 @@ def test_fast128_state_overwrite(torch_dev):
         _compare_state(fast, gen, t)
 
 
+@pytest.mark.parametrize("where", ["pool", "set_state"])
+def test_fast128_hi_bits_vs_generic(torch_dev, where):
+    """Cell bits 12-14 (no cell type uses them) on 128x128 boards: the kernel's 8-plane
+    start-board spool leaves them out, and envs whose start board may carry them
+    (spawn_flags bit 2) get the exact side-effect term from a second pass.  From pool
+    levels (the resets set the flag; start boards from the pool planes) and from boards
+    loaded by set_state (the host sets it; start boards from HBM), with the bits also
+    on board cells whose start cells lack them, against the per-cell generic kernel."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    rng = np.random.RandomState(23)
+    pool = LevelPool.load(C5_POOL)
+    if where == "pool":
+        walls = (pool.board & 0x10) != 0
+        pool.board[walls & (rng.rand(*pool.board.shape) < 0.3)] |= np.uint16(0x5000)
+        pool.board[walls & (rng.rand(*pool.board.shape) < 0.2)] |= np.uint16(0x2000)
+    B, T = 96, 40
+    kw = dict(time_limit=25, view_shape=(15, 15), output_channels=None, penalty_coef=1.0,
+              min_performance=0.01, rng="philox", seed=6, level_order="random",
+              augment_roll=True)
+    fast = SafeLifeVecEnv(pool, B, "cuda:0", kernel="fast", **kw)
+    gen = SafeLifeVecEnv(pool, B, "cuda:0", kernel="generic", **kw)
+    fast.reset()
+    gen.reset()
+    if where == "pool":
+        assert (fast.st_t["spawn_flags"].cpu().numpy() & 4).any()
+    for t in range(T):
+        a = torch.from_numpy(rng.choice(9, size=B, p=[.05] + [.1] * 4 + [.1375] * 4)
+                             .astype(np.int32)).to(dev)
+        if t == 6 and where == "set_state":
+            bd, gl, sb = (x.cpu().numpy().copy() for x in (fast.board, fast.goals,
+                                                          fast.start_board))
+            walls = (sb & 0x10) != 0
+            sb[walls & (rng.rand(*sb.shape) < 0.3)] |= np.uint16(0x3000)
+            sb[: B // 3] &= np.uint16(0x8FFF)             # a third without them
+            wb = (bd & 0x10) != 0
+            bd[wb & (rng.rand(*bd.shape) < 0.2)] |= np.uint16(0x4000)   # board side only
+            fast.set_state(bd, gl, sb)
+            gen.set_state(bd, gl, sb)
+            fl = fast.st_t["spawn_flags"].cpu().numpy()
+            assert not (fl[: B // 3] & 4).any() and (fl[B // 3:] & 4).any()
+        _, r1, d1, _ = fast.step(a)
+        _, r2, d2, _ = gen.step(a)
+        assert torch.equal(r1, r2), (t, (r1 - r2).abs().max().item())
+        assert torch.equal(d1, d2), t
+        assert torch.equal(fast.flags, gen.flags), t
+        if t % 5 == 0 or t == T - 1:
+            _compare_state(fast, gen, t)
+
+
 # ------------------------------------------------------- side-effect densities (A15)
 def test_side_effect_densities_reference_fixture(torch_dev):
     """sl_side_effect_densities in replay mode reproduces the reference's density maps
