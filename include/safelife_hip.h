@@ -203,7 +203,13 @@ typedef struct sl_env_state {
                                  power toggle, which the kernels allow for -- only
                                  moved).  The replay prologues skip the eligible
                                  count of a tensor whose bit is clear: a caller
-                                 writing state sets both bits.                 */
+                                 writing state sets both bits.
+                                 bit2: the start board may use cell bits 12-14
+                                 (no cell type does; set at reset from the level):
+                                 the 128x128 kernel keeps no start planes for them
+                                 and takes such an env's exact side-effect term in
+                                 a second pass.  A caller writing start boards
+                                 sets it where they carry those bits.          */
     int32_t *start_roll;      /* (dy << 16) | dx: start_board[b] equals pool
                                  level level_index[b] rolled by (dy, dx) (set by
                                  every reset); -1: start_board was written by
