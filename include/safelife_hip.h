@@ -204,12 +204,18 @@ typedef struct sl_env_state {
                                  moved).  The replay prologues skip the eligible
                                  count of a tensor whose bit is clear: a caller
                                  writing state sets both bits.
+                                 128x128 boards only (0 on other shapes):
                                  bit2: the start board may use cell bits 12-14
                                  (no cell type does; set at reset from the level):
                                  the 128x128 kernel keeps no start planes for them
                                  and takes such an env's exact side-effect term in
                                  a second pass.  A caller writing start boards
-                                 sets it where they carry those bits.          */
+                                 sets it where they carry those bits.
+                                 bit3: a goal cell uses bits other than alive,
+                                 destructible, frozen and colours (set at reset):
+                                 with bits 1 and 3 clear the 128x128 kernel keeps
+                                 the goals' six planes in the mirror and reads
+                                 them from there.                              */
     int32_t *start_roll;      /* (dy << 16) | dx: start_board[b] equals pool
                                  level level_index[b] rolled by (dy, dx) (set by
                                  every reset); -1: start_board was written by
@@ -231,7 +237,9 @@ typedef struct sl_env_state {
                                  a fixed point (no spawner, unchanged by the
                                  last step: the rule is skipped); bit3: the
                                  board's draw planes (elig_planes) hold its
-                                 eligible cells as the last step left them.
+                                 eligible cells as the last step left them;
+                                 bit4 (128x128): the mirror holds all six goal
+                                 planes (spawn_flags bit3), not only colours.
                                  Anything
                                  that writes the goals other than the 64x64
                                  kernel and its reset clears it.               */

@@ -221,6 +221,12 @@ __device__ __forceinline__ void pool_start_lds(const __attribute__((address_spac
     }
 }
 
+// The goal planes the mirror holds in full for goals of the usual cell types (alive,
+// destructible, frozen, colours: cell bits 0x0E19, no spawner); the colour planes 9-11
+// are kept for every env.
+constexpr int kGoalPlanes = 6;
+__device__ __forceinline__ int goal_plane(int i) { return i < 3 ? (i == 0 ? 0 : i + 2) : i + 6; }
+
 // the decided spawns of band t of a tensor (0 board, 1 goals) for the step kernel's
 // rule: loaded at the band's start, under its row loads; none when the tensor draws
 // nothing this step (`draws` false)
@@ -314,7 +320,7 @@ k_env_step_bits128(Step128KArgs ka) {
     __shared__ uint16_t slots_[kDrawSlots];
     lds_u16 *slots = (lds_u16 *)slots_;
     const int pok_all = rec(V, R_POK), pok = pok_all & 6;
-    int gok = pok;              // the goals' planes_ok bits after this step
+    int gok = pok_all & (6 | 16);   // the goals' planes_ok bits after this step
     const Scratch w = scratch_of(fx.scratch, st.B);
     // replay with draw planes: the spawns come decided from them (k_stream_draw128), for
     // the tensors that draw (scratch act[B + b] bit 0 board, bit 1 goals), and the
@@ -340,19 +346,40 @@ k_env_step_bits128(Step128KArgs ka) {
     // kept from band 0's load, and band 0's upper halo is row 127, read up front.
 
     // ---- goals: advanced band by band unless at a fixed point; the mirror keeps
-    // their planes (all words rewritten when it was stale, else the changed ones)
+    // their colour planes (all words rewritten when it was stale, else the changed
+    // ones).  Goals whose cells use only planes 0, 3, 4 and 9-11 and hold no spawner
+    // (spawn_flags bits 1 and 3 clear: the rule then creates no other bit) keep those
+    // six planes there (planes_ok bit 4) and are read back from them -- 12 of the
+    // 32 KiB of their cells, no transposes -- with the halo rows from the cells
+    const int spf = rec(V, R_SPF);
     if ((pok & 6) != 6) {
         const bool all = !(pok & 2);
+        const bool gplanes = (spf & (2 | 8)) == 0;
+        const bool from_mirror = gplanes && (pok_all & 16) && (pok & 2);
         u32 changed = 0, spawners = 0;
-        u32 up = gg[(N - 1) * RS], row0 = 0;
+        u32 up = gg[(N - 1) * RS], row0 = from_mirror ? gg[0] : 0u;
 #pragma unroll 1
         for (int t = 0; t < NB; t++) {
             u32 G[32];
-            load_pairs_nt<RS>(gg + 32 * t * RS, G);
-            const u32 dn = t < NB - 1 ? gg[(32 * t + 32) * RS] : row0;
-            if (t == 0) row0 = G[0];
-            const u32 last = G[31];
-            transpose32(G);
+            u32 dn, last;
+            if (from_mirror) {
+                const u32 *m = mg + t * MW;
+#pragma unroll
+                for (int k = 0; k < 32; k++) G[k] = 0u;
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+#pragma unroll
+                    for (int i = 0; i < kGoalPlanes; i++)
+                        PL(G, goal_plane(i), q) = m[(goal_plane(i) + 16 * q) * 64];
+                dn = t < NB - 1 ? gg[(32 * t + 32) * RS] : row0;
+                last = gg[(32 * t + 31) * RS];
+            } else {
+                load_pairs_nt<RS>(gg + 32 * t * RS, G);
+                dn = t < NB - 1 ? gg[(32 * t + 32) * RS] : row0;
+                if (t == 0) row0 = G[0];
+                last = G[31];
+                transpose32(G);
+            }
             u32 cg[2];
             GeoBand<MODE> geo{lane_now(), 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_g, 0, 0, slots};
             if (MODE == SPAWN_DECIDED) draw_planes(geo, me, 1, t, dfl & 2);
@@ -360,12 +387,19 @@ k_env_step_bits128(Step128KArgs ka) {
             pos_g += geo.used;
             up = last;
             const u32 rg = wave_or(cg[0] | cg[1]);
-            u32 *m = mg + t * MW;       // only the colour planes are ever read back
+            u32 *m = mg + t * MW;
 #pragma unroll
             for (int q = 0; q < 2; q++)
-                if (all || cg[q])
+                if (all || (!from_mirror && gplanes) || cg[q]) {
+                    if (gplanes) {
 #pragma unroll
-                    for (int k = 9; k < 12; k++) m[(k + 16 * q) * 64] = PL(G, k, q);
+                        for (int i = 0; i < kGoalPlanes; i++)
+                            m[(goal_plane(i) + 16 * q) * 64] = PL(G, goal_plane(i), q);
+                    } else {
+#pragma unroll
+                        for (int k = 9; k < 12; k++) m[(k + 16 * q) * 64] = PL(G, k, q);
+                    }
+                }
             changed |= rg;
             spawners |= PL(G, 7, 0) | PL(G, 7, 1);
             if (rg) {
@@ -378,7 +412,7 @@ k_env_step_bits128(Step128KArgs ka) {
             }
         }
         const bool fixed = changed == 0 && __ballot(spawners != 0u) == 0ull;
-        gok = 2 | (fixed ? 4 : 0);
+        gok = 2 | (fixed ? 4 : 0) | (gplanes ? 16 : 0);
         wait_vm();          // the mirror words are read back below
     }
     __builtin_amdgcn_sched_barrier(0);

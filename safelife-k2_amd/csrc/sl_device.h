@@ -23,6 +23,9 @@ constexpr uint32_t POWERS = ALIVE | INHIBIT | PRESERVE | SPAWN;
 // cell bits no cell type uses (safelife_game.py CellTypes); the 128x128 kernel keeps
 // no start-board planes for them (spawn_flags bit 2 flags a start board that has them)
 constexpr uint32_t kCellHiBits = 0x7000;
+// the cell bits the 128x128 kernel's goal plane mirror holds (alive, destructible,
+// frozen, colours); goals using any other bit set spawn_flags bit 3
+constexpr uint32_t kGoalPlaneBits = ALIVE | DESTR | FROZEN | COLORS;
 
 // ----------------------------------------------------------------------------
 // Philox4x32-10, counter (c0..c3), key = seed.  Identical to oracle/sl_oracle.c.

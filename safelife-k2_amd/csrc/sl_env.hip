@@ -448,12 +448,17 @@ k_env_exit_colors(sl_env_state st, int mode) {
 // ---------------------------------------------------------------------------
 // reset from the level pool
 // ---------------------------------------------------------------------------
+// spawn_flags bits 2 and 3 describe 128x128 boards only (the one kernel that reads
+// them); the other shapes' resets, whichever kernel runs them, leave them clear
+__device__ __forceinline__ bool is128(int H, int W) { return H == 128 && W == 128; }
+
 struct ResetShared {
     int red[NT / 64][4];
     int wave_tot[NT / 64];
     int exit_y[SL_MAX_EXITS], exit_x[SL_MAX_EXITS];
     int ev, idx, dy, dx;
     int hi;         // a start-board cell uses bits 12-14 (spawn_flags bit 2)
+    int gx;         // a goal cell uses bits outside kGoalPlaneBits (spawn_flags bit 3)
 };
 
 __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &a,
@@ -468,6 +473,7 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
         const LevelChoice c = choose_level(pool, a, gid, st.episodes[b], H, W);
         sh_idx = c.idx; sh_dy = c.dy; sh_dx = c.dx;
         sh.hi = 0;
+        sh.gx = 0;
     }
     __syncthreads();
     const int idx = sh_idx, dy = sh_dy, dx = sh_dx;
@@ -491,6 +497,7 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
             acc[2] += r;
             acc[3] += ((vb & SPAWN) ? 1 : 0) + ((vg & SPAWN) ? 65536 : 0);  // counts < 2^16
             if (vb & kCellHiBits) sh.hi = 1;
+            if (vg & ~kGoalPlaneBits) sh.gx = 1;
             ex = (vb & EXIT) != 0;
         }
         int tot;
@@ -504,7 +511,7 @@ __device__ void reset_one(const sl_env_state &st, const sl_level_pool &pool, con
     block_sum4(acc, red);
     if (threadIdx.x == 0) {
         const int spawn_bits = ((acc[3] & 0xFFFF) ? 1 : 0) | ((acc[3] >> 16) ? 2 : 0) |
-                               (sh.hi ? 4 : 0);
+                               (is128(H, W) ? (sh.hi ? 4 : 0) | (sh.gx ? 8 : 0) : 0);
         sh_ev = reset_scalars(st, pool, a, b, idx, dy, dx, acc[0], acc[1], acc[2], spawn_bits);
         st.exit_count[b] = n_exit;
         for (int e = 0; e < SL_MAX_EXITS; e++) {
@@ -537,6 +544,7 @@ struct WideResetShared {
     int exl[kExitCap];
     int nex, ev, idx, dy, dx;
     int hi;         // a start-board cell uses bits 12-14 (spawn_flags bit 2)
+    int gx;         // a goal cell uses bits outside kGoalPlaneBits (spawn_flags bit 3)
 };
 
 __device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &a,
@@ -555,6 +563,7 @@ __device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, co
             sh.dx = c.dx;
             sh.nex = 0;
             sh.hi = 0;
+            sh.gx = 0;
         }
     }
     __syncthreads();
@@ -574,6 +583,7 @@ __device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, co
         acc[2] += r;
         acc[3] += ((vb & SPAWN) ? 1 : 0) + ((vg & SPAWN) ? 65536 : 0);
         if (vb & kCellHiBits) sh.hi = 1;
+        if (vg & ~kGoalPlaneBits) sh.gx = 1;
         if (vb & EXIT) {
             const int k = atomicAdd(&sh.nex, 1);
             if (k < kExitCap) sh.exl[k] = i;
@@ -589,7 +599,7 @@ __device__ void reset_wide(const sl_env_state &st, const sl_level_pool &pool, co
         for (int w = 0; w < NTR / 64; w++)
             for (int k = 0; k < 4; k++) t[k] += sh.red[w][k];
         const int spawn_bits = ((t[3] & 0xFFFF) ? 1 : 0) | ((t[3] >> 16) ? 2 : 0) |
-                               (sh.hi ? 4 : 0);
+                               (is128(H, W) ? (sh.hi ? 4 : 0) | (sh.gx ? 8 : 0) : 0);
         sh.ev = reset_scalars_from(st, a, b, idx, dy, dx, ls, ep, t[0], t[1], t[2], spawn_bits);
         const int nex = sh.nex;
         int16_t *ey = st.exit_y + b * SL_MAX_EXITS, *ex = st.exit_x + b * SL_MAX_EXITS;

@@ -254,7 +254,8 @@ __device__ __forceinline__ uint16_t reset_scalars_from(const sl_env_state &st, c
 // SimpleSideEffectPenalty.reset, env_wrappers.py:90-94,313-317).  One thread.
 //   points / base / possible: sums over the (rolled) initial board and goals;
 //   spawn_bits: bit0 board, bit1 goals hold a spawning cell; bit2 a start-board cell
-//   uses bits 12-14 (no cell type does; the 128x128 kernel's spool leaves them out).
+//   uses bits 12-14 (no cell type does; the 128x128 kernel's spool leaves them out);
+//   bit3 a goal cell uses bits outside kGoalPlaneBits (no goal plane mirror).
 //   Returns the exit
 //   cell value the reset board carries (update_exit_colors after revert).
 __device__ __forceinline__ uint16_t reset_scalars(const sl_env_state &st,
@@ -281,7 +282,7 @@ __device__ __forceinline__ uint16_t reset_scalars_from(const sl_env_state &st, c
     st.orientation[b] = ls.orientation;
     st.game_over[b] = 0;
     st.num_steps[b] = 0;
-    st.spawn_flags[b] = ((spawn_bits & 1) || a.toggle_powers ? 1 : 0) | (spawn_bits & 6);
+    st.spawn_flags[b] = ((spawn_bits & 1) || a.toggle_powers ? 1 : 0) | (spawn_bits & 14);
     st.episode_length[b] = 0;
     st.episode_reward[b] = 0;
     st.old_points[b] = points;

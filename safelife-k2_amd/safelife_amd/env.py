@@ -425,7 +425,8 @@ class SafeLifeGame:
             v.start_board[i].copy_(keep_start[0])
             v.state["baseline"][i] = keep_start[1]
             # spawn_flags bit 2 follows the start board kept (cell bits 12-14)
-            hi = 4 if bool(start_board_hi_bits(v.start_board[i:i + 1])[0]) else 0
+            hi = 4 if ((v.H, v.W) == (128, 128)
+                       and bool(start_board_hi_bits(v.start_board[i:i + 1])[0])) else 0
             self._set("spawn_flags", (self._st("spawn_flags") & ~4) | hi)
         # the raw level cells (the reset coloured the exits by can_exit)
         _lib.check(_lib.lib().sl_env_exit_colors(ctypes.byref(self._slice()), 1, self._stream()),

@@ -490,10 +490,10 @@ class SafeLifeVecEnv:
         longer match pool levels (kernels read them from HBM), the bit-plane
         mirrors are stale and the reset lists start empty."""
         self.st_t["start_roll"].fill_(-1)
-        # may hold spawners (replay counts them); bit 2: the start board uses cell bits
-        # 12-14, which the 128x128 kernel then compares in a second pass
-        self.st_t["spawn_flags"].copy_(3 | 4 * start_board_hi_bits(self.start_board).to(
-            self.st_t["spawn_flags"].dtype))
+        # may hold spawners (replay counts them); bit 2 (128x128 boards): the start board
+        # uses cell bits 12-14, which the 128x128 kernel then compares in a second pass
+        hi = start_board_hi_bits(self.start_board) & ((self.H, self.W) == (128, 128))
+        self.st_t["spawn_flags"].copy_(3 | 4 * hi.to(self.st_t["spawn_flags"].dtype))
         self._may_spawn = True
         self.planes_ok.zero_()
         self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()

@@ -595,14 +595,24 @@ def test_c_abi_rejects_bad_arguments(torch_dev):
 C5_POOL = os.path.join(GOLDEN, "pools", "c5_navigation_128.npz")
 
 
-def test_fast128_vs_generic(torch_dev):
+@pytest.mark.parametrize("goal_bits", [False, True])
+def test_fast128_vs_generic(torch_dev, goal_bits):
     """The 128x128 banded bit-sliced kernel against the per-cell generic kernel on the
     C5 navigation levels (spawners everywhere, oscillating goals in level 3): rewards,
-    done, flags, observations every step, all state every few steps, across resets."""
+    done, flags, observations every step, all state every few steps, across resets.
+    goal_bits: two levels' goals also carry preserve / inhibit cells (outside the goal
+    plane mirror: spawn_flags bit 3, their goals are read as cells), the other two use
+    the mirror's six planes."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
     pool = LevelPool.load(C5_POOL)
     rng = np.random.RandomState(17)
+    if goal_bits:
+        for k in (1, 3):
+            g = pool.goals[k]
+            life = (g & 0x1) != 0
+            g[life & (rng.rand(*g.shape) < 0.1)] |= np.uint16(0x20)
+            g[(g == 0) & (rng.rand(*g.shape) < 0.01)] = np.uint16(0x40 | 0x10)
     B, T = 160, 90
     kw = dict(time_limit=35, view_shape=(33, 33), output_channels=None, penalty_coef=0.7,
               min_performance=0.01, rng="philox", seed=77, level_order="random",
