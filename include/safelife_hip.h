@@ -239,7 +239,11 @@ typedef struct sl_env_state {
                                  board's draw planes (elig_planes) hold its
                                  eligible cells as the last step left them;
                                  bit4 (128x128): the mirror holds all six goal
-                                 planes (spawn_flags bit3), not only colours.
+                                 planes (spawn_flags bit3), not only colours;
+                                 bit5 (128x128): the goals are the pool level's,
+                                 as reset (set by the reset, cleared by the first
+                                 change): their colours come from the pool's
+                                 goal_planes.
                                  Anything
                                  that writes the goals other than the 64x64
                                  kernel and its reset clears it.               */
@@ -273,6 +277,12 @@ typedef struct sl_level_pool {
                                  128x128 pools: uint32 [K,16,4,W] (8*K*16*W
                                  bytes), element [k][p][q][x] bit r = bit p of
                                  board[k][32q + r][x]                          */
+    uint32_t *goal_planes;    /* 128x128 pools: the goals' colour planes, uint32
+                                 [K,3,4,W], element [k][c][q][x] bit r = bit 9+c
+                                 of goals[k][32q + r][x]; or NULL.  The 128x128
+                                 kernel scores goals still as the level had them
+                                 from here (cache-resident) instead of the
+                                 env's mirror (sl_level_pool_prepare fills it) */
 } sl_level_pool;
 
 /* Fill pool->board_planes (caller-allocated, dev, layout above; H must be 64 or

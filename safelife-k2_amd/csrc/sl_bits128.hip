@@ -320,7 +320,7 @@ k_env_step_bits128(Step128KArgs ka) {
     __shared__ uint16_t slots_[kDrawSlots];
     lds_u16 *slots = (lds_u16 *)slots_;
     const int pok_all = rec(V, R_POK), pok = pok_all & 6;
-    int gok = pok_all & (6 | 16);   // the goals' planes_ok bits after this step
+    int gok = pok_all & (6 | 16 | 32);   // the goals' planes_ok bits after this step
     const Scratch w = scratch_of(fx.scratch, st.B);
     // replay with draw planes: the spawns come decided from them (k_stream_draw128), for
     // the tensors that draw (scratch act[B + b] bit 0 board, bit 1 goals), and the
@@ -412,7 +412,7 @@ k_env_step_bits128(Step128KArgs ka) {
             }
         }
         const bool fixed = changed == 0 && __ballot(spawners != 0u) == 0ull;
-        gok = 2 | (fixed ? 4 : 0) | (gplanes ? 16 : 0);
+        gok = 2 | (fixed ? 4 : 0) | (gplanes ? 16 : 0) | (changed == 0 ? pok_all & 32 : 0);
         wait_vm();          // the mirror words are read back below
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -429,6 +429,10 @@ k_env_step_bits128(Step128KArgs ka) {
                     (int64_t)(roll >= 0 ? rec(V, R_LI) : 0) * (16 * NB * N);
     const int sdy = roll < 0 ? 0 : roll >> 16, sdx = roll < 0 ? 0 : roll & 0xFFFF;
     const bool start_hi = (rec(V, R_SPF) & 4) != 0;     // start board may use bits 12-14
+    // goals still the level's (planes_ok bit 5, after this step's goals): their colour
+    // planes from the pool (cache-resident) instead of the mirror (HBM)
+    const u32 *gp = (roll >= 0 && (gok & 32) && pool.goal_planes)
+                        ? pool.goal_planes + (int64_t)rec(V, R_LI) * (3 * NB * N) : nullptr;
     int pts = 0, scr = 0, pos = 0, side = 0;
     u32 up = gb[(N - 1) * RS], row0 = 0;
     // SPAWN_DECIDED: the eligibility planes of the previous band (of band 0 in LDS, in
@@ -475,11 +479,23 @@ k_env_step_bits128(Step128KArgs ka) {
         }
         __builtin_amdgcn_sched_barrier(0);
         u32 gcol[3][2];
-        const u32 *m = mg + t * MW;
+        if (gp) {       // the rolled level's band: two level words and a funnel shift
+            const int r0 = (32 * t - sdy) & (N - 1), q0 = r0 >> 5, q1 = (q0 + 1) & (NB - 1);
+            const u32 sh = (u32)(r0 & 31);
+            const int c0 = (2 * lane_now() - sdx) & (N - 1), c1 = (c0 + 1) & (N - 1);
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            gcol[k][0] = m[(9 + k) * 64];
-            gcol[k][1] = m[(25 + k) * 64];
+            for (int k = 0; k < 3; k++) {
+                const u32 *g0 = gp + (k * NB + q0) * N, *g1 = gp + (k * NB + q1) * N;
+                gcol[k][0] = __builtin_amdgcn_alignbit(g1[c0], g0[c0], sh);
+                gcol[k][1] = __builtin_amdgcn_alignbit(g1[c1], g0[c1], sh);
+            }
+        } else {
+            const u32 *m = mg + t * MW;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                gcol[k][0] = m[(9 + k) * 64];
+                gcol[k][1] = m[(25 + k) * 64];
+            }
         }
         int p, q, r, e;
         u32 S[32];

@@ -702,6 +702,24 @@ __global__ void __launch_bounds__(NT) k_pool_planes(sl_level_pool pool) {
     }
 }
 
+// pool->goal_planes (H == 128): 32-bit words [k][c][q][x] bit r = bit 9 + c of
+// pool->goals[k][32q + r][x]
+__global__ void __launch_bounds__(NT) k_pool_goal_planes(sl_level_pool pool) {
+    const int nq = pool.H / 32;
+    const int64_t n = (int64_t)pool.K * 3 * nq * pool.W;
+    for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+        const int64_t k = i / (3 * nq * pool.W);
+        int r = (int)(i - k * 3 * nq * pool.W);
+        const int c = r / (nq * pool.W);
+        r -= c * nq * pool.W;
+        const int q = r / pool.W, x = r - q * pool.W;
+        const uint16_t *gd = pool.goals + (k * pool.H + 32 * q) * pool.W + x;
+        uint32_t v = 0;
+        for (int y = 0; y < 32; y++) v |= (uint32_t)((gd[y * pool.W] >> (9 + c)) & 1u) << y;
+        pool.goal_planes[i] = v;
+    }
+}
+
 // explicit resets (mask or all envs): grid-stride over envs, one block per env
 __global__ void __launch_bounds__(NT)
 k_env_reset(sl_env_state st, sl_level_pool pool, const uint8_t *__restrict__ mask,
@@ -1058,6 +1076,12 @@ extern "C" int sl_level_pool_prepare(sl_level_pool *pool, void *stream) {
     const int64_t n = (int64_t)pool->K * 16 * (pool->H / 32) * pool->W;
     const unsigned grid = (unsigned)std::min<int64_t>((n + NT - 1) / NT, 4096);
     hipLaunchKernelGGL(k_pool_planes, dim3(grid), dim3(NT), 0, (hipStream_t)stream, *pool);
+    if (pool->goal_planes && pool->H == 128) {
+        if (!pool->goals) return SL_EINVAL;
+        const int64_t ng = (int64_t)pool->K * 3 * (pool->H / 32) * pool->W;
+        const unsigned gg = (unsigned)std::min<int64_t>((ng + NT - 1) / NT, 4096);
+        hipLaunchKernelGGL(k_pool_goal_planes, dim3(gg), dim3(NT), 0, (hipStream_t)stream, *pool);
+    }
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 

@@ -298,7 +298,8 @@ __device__ __forceinline__ uint16_t reset_scalars_from(const sl_env_state &st, c
     st.prior_head[b] = 0;
     st.level_index[b] = idx;
     if (st.start_roll) st.start_roll[b] = (dy << 16) | dx;
-    if (st.planes_ok) st.planes_ok[b] = 0;    // the 64x64 reset re-validates
+    // the 64x64 reset re-validates; a 128x128 env's goals are the level's (bit 5)
+    if (st.planes_ok) st.planes_ok[b] = (H == 128 && W == 128) ? 32 : 0;
     st.episodes[b] = ep + 1;
     return (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
 }

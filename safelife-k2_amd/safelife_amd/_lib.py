@@ -50,7 +50,7 @@ class LevelPool(ctypes.Structure):
     _fields_ = [("K", i32), ("H", i32), ("W", i32),
                 ("board", vp), ("goals", vp), ("agent_x", vp), ("agent_y", vp),
                 ("orientation", vp), ("spawn_prob", vp), ("min_performance", vp),
-                ("board_planes", vp)]
+                ("board_planes", vp), ("goal_planes", vp)]
 
 
 class EnvCfg(ctypes.Structure):

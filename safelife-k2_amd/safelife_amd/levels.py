@@ -133,6 +133,10 @@ class LevelPool:
             t["board_planes"] = torch.empty((self.K, 16, self.H // 32, self.W),
                                             dtype=torch.int32, device=device)
             s.board_planes = t["board_planes"].data_ptr()
+            if self.H == 128:      # the goals' colour planes, uint32 [K,3,4,W]
+                t["goal_planes"] = torch.empty((self.K, 3, self.H // 32, self.W),
+                                               dtype=torch.int32, device=device)
+                s.goal_planes = t["goal_planes"].data_ptr()
             L = _lib.lib()
             _lib.check(L.sl_level_pool_prepare(ctypes.byref(s), _lib.stream_ptr(device)),
                        "sl_level_pool_prepare")
