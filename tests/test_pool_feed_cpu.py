@@ -77,3 +77,23 @@ def test_level_pool_exit_cap():
     board[0, 15, 15] = 272
     with pytest.raises(ValueError, match="exits"):
         LevelPool(board, goals, [(0, 0)], [0], [0.3], [0.01])
+
+
+def test_start_board_hi_bits_and_pool_cell_bits():
+    """spawn_flags bit 2's host side (start boards using the unused cell bits 12-14) and
+    what the 128x128 kernel's bit-2 / bit-3 paths assume of the benchmark pools: no
+    level uses bits 12-14, and the C5 goals use only alive, destructible, frozen and
+    colour bits (the goal plane mirror's 0x0E19) and hold no spawner."""
+    import torch
+    from safelife_amd.vec_env import start_board_hi_bits
+    sb = torch.zeros((3, 8, 8), dtype=torch.int16)       # the uint16 boards' bits
+    sb[1, 2, 3] = 0x1010
+    sb[2, 7, 7] = -0x7FF0          # 0x8010: the pullable bit, not 12-14
+    assert start_board_hi_bits(sb).tolist() == [False, True, False]
+    pools = os.path.join(os.path.dirname(__file__), "golden", "pools")
+    for name in ("c2_append_still_25", "c3_prune_still_64", "c4_append_still_64",
+                 "c5_navigation_128"):
+        p = LevelPool.load(os.path.join(pools, name + ".npz"))
+        assert not ((p.board & 0x7000) != 0).any(), name
+    c5 = LevelPool.load(os.path.join(pools, "c5_navigation_128.npz"))
+    assert not (c5.goals & ~np.uint16(0x0E19)).any()
