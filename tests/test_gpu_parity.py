@@ -741,6 +741,43 @@ def test_fast128_hi_bits_vs_generic(torch_dev, where):
             _compare_state(fast, gen, t)
 
 
+def test_fast128_pool_swap_vs_generic(torch_dev):
+    """A pool swap mid-run on 128x128 boards: running episodes stop reading their start
+    planes and pristine goal colours from the pool (start_roll = -1: start boards and
+    the goals mirror from HBM) until they are reset from the new pool, against the
+    per-cell generic kernel, across the swap and the resets after it."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    pool = LevelPool.load(C5_POOL)
+    perm = [2, 0, 3, 1]
+    al = np.stack([pool.agent_x, pool.agent_y], 1)
+    pool2 = LevelPool(np.roll(pool.board[perm], 5, axis=2), np.roll(pool.goals[perm], 5, axis=2),
+                      (al[perm] + [5, 0]) % 128, pool.orientation[perm], pool.spawn_prob[perm],
+                      pool.min_performance[perm])
+    rng = np.random.RandomState(31)
+    B, T = 96, 50
+    kw = dict(time_limit=20, view_shape=(15, 15), output_channels=None, penalty_coef=1.0,
+              min_performance=0.01, rng="philox", seed=9, level_order="random",
+              augment_roll=True)
+    fast = SafeLifeVecEnv(pool, B, "cuda:0", kernel="fast", **kw)
+    gen = SafeLifeVecEnv(pool, B, "cuda:0", kernel="generic", **kw)
+    fast.reset()
+    gen.reset()
+    for t in range(T):
+        if t == 13:
+            fast.set_pool(pool2)
+            gen.set_pool(pool2)
+        a = torch.from_numpy(rng.choice(9, size=B, p=[.05] + [.1] * 4 + [.1375] * 4)
+                             .astype(np.int32)).to(dev)
+        _, r1, d1, _ = fast.step(a)
+        _, r2, d2, _ = gen.step(a)
+        assert torch.equal(r1, r2), (t, (r1 - r2).abs().max().item())
+        assert torch.equal(d1, d2), t
+        assert torch.equal(fast.flags, gen.flags), t
+        if t % 4 == 0 or t == T - 1:
+            _compare_state(fast, gen, t)
+
+
 # ------------------------------------------------------- side-effect densities (A15)
 def test_side_effect_densities_reference_fixture(torch_dev):
     """sl_side_effect_densities in replay mode reproduces the reference's density maps
