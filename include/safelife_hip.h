@@ -117,6 +117,58 @@ int sl_count_eligible(const uint16_t *in, int64_t *counts, int64_t B, int H, int
 int sl_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n,
                           const int64_t *base, int64_t *total_out, void *stream);
 
+/* -------------------------------------------- seeded reference stream -- */
+
+/*
+ * The reference's spawn stream on the device: numpy's legacy RandomState(seed)
+ * .random_sample() -- MT19937 seeded by init_genrand, doubles (a >> 5, b >> 6) / 2^53
+ * from consecutive outputs -- which speedups.seed(seed) makes the reference draw
+ * from in 10 000-double chunks (speedups_src/random.c:14-26,28-44,47-52,
+ * module.c:246-253).  Draw d lands in ring[d & (ring_draws - 1)].
+ *
+ * The stream is cut into blocks of 624 * rounds raw outputs (312 * rounds draws);
+ * block q is generated by chain q mod n_chains, whose state then jumps n_chains
+ * blocks ahead (x^(n_chains * block) mod the characteristic polynomial, applied
+ * to the block's own first raw words).  All buffers are caller-allocated device
+ * memory:
+ *   chains   uint32 [n_chains, 624]          the MT state of each chain's next block
+ *   prefix   uint32 [n_chains, SL_MT_PREFIX] scratch
+ *   polys    uint32 [log2(n_chains) + 1, SL_MT_POLY_WORDS] jump polynomials
+ *   ctl      int64 [4]: next block to generate, a done counter, error flags (bit0:
+ *            a fill asked for a range the ring or the chains cannot serve), the
+ *            first block
+ * n_chains is a power of two (one fill generates at most n_chains blocks), rounds
+ * >= 33, ring_draws a power of two >= 2 blocks.
+ */
+#define SL_MT_PREFIX 21216       /* 34 x 624 raw words */
+#define SL_MT_POLY_WORDS 640
+typedef struct sl_mt19937 {
+    int32_t n_chains;
+    int32_t rounds;
+    int64_t ring_draws;
+    double *ring;
+    uint32_t *chains;
+    uint32_t *prefix;
+    uint32_t *polys;
+    int64_t *ctl;
+} sl_mt19937;
+
+/* Seed: the stream of RandomState(seed), positioned so that draws from first_draw
+ * on can be generated (host polynomial work, then device init; synchronises
+ * `stream`).  Re-seed to move the position backwards. */
+int sl_mt19937_seed(sl_mt19937 *mt, uint32_t seed, int64_t first_draw, void *stream);
+/* Generate every not yet generated block holding a draw below *hi (dev int64);
+ * *lo (dev) is the first draw the caller will read.  err (dev int64, may be NULL)
+ * is OR-ed with 1 when the range cannot be served (re-seed). */
+int sl_mt19937_fill(const sl_mt19937 *mt, const int64_t *lo, const int64_t *hi, int64_t *err,
+                    void *stream);
+/* Host reference pieces (no GPU): the seeded window, x^n mod phi, a jump of a
+ * window by a polynomial, and n draws from a window (tests; seeding). */
+int sl_mt19937_host_window(uint32_t seed, uint32_t *window624);
+int sl_mt19937_host_jump_poly(uint64_t n, uint32_t *poly);
+int sl_mt19937_host_jump(const uint32_t *window_in, const uint32_t *poly, uint32_t *window_out);
+int sl_mt19937_host_draws(const uint32_t *window, int64_t n, double *out);
+
 /* ------------------------------------------------------- side effects -- */
 
 /*
@@ -369,6 +421,13 @@ typedef struct sl_env_cfg {
                                        step completes, *stream_pos = *stream_base
                                        + the batch's total                     */
     const int64_t *stream_base;     /* dev [1]: phase 2's first uniform        */
+    const sl_mt19937 *mt;           /* SL_RNG_STREAM: host pointer or NULL.  When
+                                       set, the draws come from this device
+                                       generator's ring (draws / n_draws are not
+                                       read): after the offsets scan each step
+                                       fills it for the step's range, so the
+                                       stream is RandomState(seed) from
+                                       *stream_pos on with no host buffer      */
 } sl_env_cfg;
 
 /*

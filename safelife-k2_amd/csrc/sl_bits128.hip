@@ -333,7 +333,7 @@ k_env_step_bits128(Step128KArgs ka) {
     sc.step = a.step;
     sc.seed = a.seed;
     set_spawn_prob(sc, __int_as_float(rec(V, R_SPAWN)));
-    StreamSrc ssrc{a.draws, a.n_draws, nullptr};
+    StreamSrc ssrc{a.draws, a.n_draws, nullptr, a.draw_mask};
     int64_t pos_b = 0, pos_g = 0;
     if (MODE == SPAWN_STREAM) {
         ssrc.err = w.err;
@@ -754,7 +754,7 @@ __device__ __forceinline__ void draw_env128(const Step128KArgs &ka, int64_t b, i
     lds_u32 *spw = (lds_u32 *)spw_;
     const double thr = (double)st.spawn_prob[b];
     const double *draws = ka.a.draws;
-    const int64_t n_draws = ka.a.n_draws;
+    const int64_t n_draws = ka.a.n_draws, draw_mask = ka.a.draw_mask;
     u32 *dp = st.elig_planes + b * kEligStride + kDrawPlanes + lane;
 #pragma unroll 1
     for (int tensor = 0; tensor < 2; tensor++) {
@@ -820,7 +820,7 @@ __device__ __forceinline__ void draw_env128(const Step128KArgs &ka, int64_t b, i
                     const int i = i0 + 64 * k + lane;
                     const int64_t r = pos + c0 + i;
                     id[k] = i < n ? (u32)slots[i] : 0u;
-                    u[k] = (i < n && r < n_draws) ? draws[r] : 1.0;
+                    u[k] = (i < n && r < n_draws) ? draws[r & draw_mask] : 1.0;
                     if (i < n && r >= n_draws) atomicOr((unsigned long long *)w.err, 1ull);
                 }
 #pragma unroll

@@ -287,13 +287,13 @@ k_env_step_generic(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
             if (eb) {
                 if (thr <= 0.0) ub = 1.0;
                 else if (thr >= 1.0) ub = 0.0;
-                else if (pos_b + rb < a.n_draws) ub = a.draws[pos_b + rb];
+                else if (pos_b + rb < a.n_draws) ub = a.draws[(pos_b + rb) & a.draw_mask];
                 else atomicOr((unsigned long long *)err, 1ull);
             }
             if (eg) {
                 if (thr <= 0.0) ug = 1.0;
                 else if (thr >= 1.0) ug = 0.0;
-                else if (pos_g + rg < a.n_draws) ug = a.draws[pos_g + rg];
+                else if (pos_g + rg < a.n_draws) ug = a.draws[(pos_g + rg) & a.draw_mask];
                 else atomicOr((unsigned long long *)err, 1ull);
             }
             pos_b += tb;
@@ -370,13 +370,13 @@ k_env_advance(sl_env_state st, StepArgs a, const int64_t *__restrict__ offsets,
             if (eb) {
                 if (thr <= 0.0) ub = 1.0;
                 else if (thr >= 1.0) ub = 0.0;
-                else if (pos_b + rb < a.n_draws) ub = a.draws[pos_b + rb];
+                else if (pos_b + rb < a.n_draws) ub = a.draws[(pos_b + rb) & a.draw_mask];
                 else atomicOr((unsigned long long *)err, 1ull);
             }
             if (eg) {
                 if (thr <= 0.0) ug = 1.0;
                 else if (thr >= 1.0) ug = 0.0;
-                else if (pos_g + rg < a.n_draws) ug = a.draws[pos_g + rg];
+                else if (pos_g + rg < a.n_draws) ug = a.draws[(pos_g + rg) & a.draw_mask];
                 else atomicOr((unsigned long long *)err, 1ull);
             }
             pos_b += tb;
@@ -1091,7 +1091,11 @@ int sl::stream_offsets(const sl_env_state &st, const FastExtra &fx, hipStream_t 
     // in *stream_pos); 2: from the shard's base the caller placed in *stream_base
     const int64_t *base = fx.stream_phase == 1 ? nullptr
                           : fx.stream_phase == 2 ? fx.stream_base : fx.stream_pos;
-    return sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * st.B, base, fx.stream_pos, (void *)s);
+    const int rc = sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * st.B, base, fx.stream_pos,
+                                         (void *)s);
+    // the device generator: every block holding a draw of [offsets[0], *stream_pos)
+    if (rc || !fx.mt || fx.stream_phase == 1) return rc;
+    return sl_mt19937_fill(fx.mt, sc.offsets, fx.stream_pos, sc.err, (void *)s);
 }
 
 extern "C" int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const uint8_t *mask,
@@ -1135,7 +1139,12 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
 
     if (cfg->rng_mode != SL_RNG_STREAM && cfg->rng_mode != SL_RNG_PHILOX) return SL_EINVAL;
     const bool replay = cfg->rng_mode == SL_RNG_STREAM;
-    if (replay && (!cfg->stream_pos || (!cfg->draws && cfg->n_draws > 0))) return SL_EINVAL;
+    if (replay && cfg->mt) {       // draws from the device generator's ring
+        a.draws = cfg->mt->ring;
+        a.n_draws = INT64_MAX;
+        a.draw_mask = cfg->mt->ring_draws - 1;
+    }
+    if (replay && (!cfg->stream_pos || (!a.draws && a.n_draws > 0))) return SL_EINVAL;
     if (cfg->stream_phase < 0 || cfg->stream_phase > 2 || (cfg->stream_phase && !replay) ||
         (cfg->stream_phase == 2 && !cfg->stream_base))
         return SL_EINVAL;
@@ -1162,6 +1171,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     fx.stream_pos = cfg->stream_pos;
     fx.stream_phase = cfg->stream_phase;
     fx.stream_base = cfg->stream_base;
+    fx.mt = replay ? cfg->mt : nullptr;
     fx.ev_begin = cfg->ev_begin;
     // the small-board kernel resets finished envs inside the step; with a capture the
     // resets run in the follow-up scan so the pre-reset frame can be copied first.
@@ -1311,7 +1321,9 @@ extern "C" int sl_env_advance(sl_env_state *st, const sl_env_cfg *cfg, void *str
     if (!state_ok(st) || !cfg || !cfg->scratch) return SL_EINVAL;
     if (cfg->rng_mode != SL_RNG_STREAM && cfg->rng_mode != SL_RNG_PHILOX) return SL_EINVAL;
     const bool replay = cfg->rng_mode == SL_RNG_STREAM;
-    if (replay && (!cfg->stream_pos || (!cfg->draws && cfg->n_draws > 0))) return SL_EINVAL;
+    if (replay && !cfg->mt && (!cfg->stream_pos || (!cfg->draws && cfg->n_draws > 0)))
+        return SL_EINVAL;
+    if (replay && !cfg->stream_pos) return SL_EINVAL;
     const int64_t B = st->B;
     if (B == 0) return SL_OK;
     hipStream_t s = (hipStream_t)stream;
@@ -1323,12 +1335,18 @@ extern "C" int sl_env_advance(sl_env_state *st, const sl_env_cfg *cfg, void *str
     a.env0 = cfg->env0;
     a.draws = cfg->draws;
     a.n_draws = cfg->n_draws;
+    if (replay && cfg->mt) {
+        a.draws = cfg->mt->ring;
+        a.n_draws = INT64_MAX;
+        a.draw_mask = cfg->mt->ring_draws - 1;
+    }
     if (replay) {
         if (!set_lds((const void *)k_env_count, lds)) return SL_ETOOBIG;
         hipLaunchKernelGGL(k_env_count, dim3((unsigned)B), dim3(NT), lds, s, *st, sc.counts);
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
-        const int rc = sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * B, cfg->stream_pos,
-                                             cfg->stream_pos, stream);
+        int rc = sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * B, cfg->stream_pos,
+                                       cfg->stream_pos, stream);
+        if (!rc && cfg->mt) rc = sl_mt19937_fill(cfg->mt, sc.offsets, cfg->stream_pos, sc.err, stream);
         if (rc) return rc;
         if (!set_lds((const void *)k_env_advance<SL_RNG_STREAM>, lds)) return SL_ETOOBIG;
         hipLaunchKernelGGL(k_env_advance<SL_RNG_STREAM>, dim3((unsigned)B), dim3(NT), lds, s,

@@ -45,6 +45,8 @@ struct StepArgs {
     uint32_t step, env0;
     const double *draws;
     int64_t n_draws;
+    int64_t draw_mask = -1;      // draw r is draws[r & draw_mask]: -1 for a linear buffer,
+                                 // ring_draws - 1 for the device generator's ring (sl_mt.hip)
 };
 
 __device__ __forceinline__ int pymod(int a, int m) {
@@ -324,6 +326,8 @@ struct FastExtra {
     int32_t stream_phase;   // replay split over shards (sl_env_cfg.stream_phase): 0
                             // whole step, 1 action + counts + total, 2 offsets from
     const int64_t *stream_base;   // *stream_base + the step
+    const sl_mt19937 *mt;   // replay from the device generator (sl_env_cfg.mt) or NULL:
+                            // stream_offsets fills its ring for the step's range
 };
 // replay-mode phases of a bit-sliced launcher: whether it runs the action + count
 // prologue, and whether it continues past the offsets scan to the step kernel

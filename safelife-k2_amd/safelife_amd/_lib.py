@@ -64,7 +64,12 @@ class EnvCfg(ctypes.Structure):
                 ("ev_begin", vp), ("ev_end", vp), ("kernel", i32),
                 ("obs_out", vp), ("obs_mode", i32), ("obs_vh", i32), ("obs_vw", i32),
                 ("obs_remove_white", i32), ("obs_nch", i32), ("obs_channels", i32 * 16),
-                ("capture", vp), ("stream_phase", i32), ("stream_base", vp)]
+                ("capture", vp), ("stream_phase", i32), ("stream_base", vp), ("mt", vp)]
+
+
+class MT19937(ctypes.Structure):
+    _fields_ = [("n_chains", i32), ("rounds", i32), ("ring_draws", i64), ("ring", vp),
+                ("chains", vp), ("prefix", vp), ("polys", vp), ("ctl", vp)]
 
 
 class Capture(ctypes.Structure):
@@ -126,6 +131,16 @@ def lib():
             "sl_env_exit_colors": [ctypes.POINTER(EnvState), ctypes.c_int, vp]}
     for name, args in game.items():
         # (an A/B build of an older revision, SAFELIFE_HIP_LIB, may lack these)
+        if hasattr(L, name) or LIB_PATH == _DEFAULT_LIB:
+            getattr(L, name).argtypes = args
+            getattr(L, name).restype = ctypes.c_int
+    mt = {"sl_mt19937_seed": [ctypes.POINTER(MT19937), u32, i64, vp],
+          "sl_mt19937_fill": [ctypes.POINTER(MT19937), vp, vp, vp, vp],
+          "sl_mt19937_host_window": [u32, vp],
+          "sl_mt19937_host_jump_poly": [u64, vp],
+          "sl_mt19937_host_jump": [vp, vp, vp],
+          "sl_mt19937_host_draws": [vp, i64, vp]}
+    for name, args in mt.items():
         if hasattr(L, name) or LIB_PATH == _DEFAULT_LIB:
             getattr(L, name).argtypes = args
             getattr(L, name).restype = ctypes.c_int

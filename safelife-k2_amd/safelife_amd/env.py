@@ -546,6 +546,9 @@ class SafeLifeEnv:
     def reset(self):
         venv = self._env_for(next(self.level_iterator))
         venv.reset()
+        self._frame()
+        venv.stream_pos.zero_()
+        self._stream_at = 0
         self.game = SafeLifeGame(venv)
         self.episode_length = 0
         self.episode_reward = 0
@@ -554,28 +557,81 @@ class SafeLifeEnv:
             self.global_counter.episodes_started += 1
         return self.get_obs()
 
+    def _frame(self):
+        """Per-env staging for step(): pinned host buffers and one device frame, so a
+        step is one upload (action, staged draws), the step kernels, one gather kernel
+        into the frame (obs, reward, flags, stream position, board, goals, agent) and
+        one download -- a single host sync."""
+        v = self._venv
+        if getattr(self, "_frame_env", None) is v:
+            return self._frame_data
+        torch = v.torch
+        parts = [v.obs[0:1], v.reward, v.flags, v.stream_pos, v.board[0:1], v.goals[0:1],
+                 v.st_t["agent_x"], v.st_t["agent_y"]]
+        views = [p.reshape(-1).view(torch.uint8) for p in parts]
+        offs = np.cumsum([0] + [x.numel() for x in views])
+        n2 = 2 * v.H * v.W
+        fr = {"views": views, "offs": offs,
+              "dev": torch.empty(int(offs[-1]), dtype=torch.uint8, device=v.device),
+              "host": torch.empty(int(offs[-1]), dtype=torch.uint8, pin_memory=True),
+              "act_h": torch.empty(1, dtype=torch.int32, pin_memory=True),
+              "draws_h": torch.empty(n2, dtype=torch.float64, pin_memory=True),
+              "draws_d": torch.empty(n2, dtype=torch.float64, device=v.device)}
+        fr["host_np"] = fr["host"].numpy()
+        # (bfloat16 views come back as their raw 16-bit words: numpy has no bfloat16)
+        fr["obs_dtype"] = {torch.uint16: np.uint16, torch.uint8: np.uint8,
+                           torch.float32: np.float32}.get(v.obs.dtype, np.uint16)
+        if self.rng == "reference":
+            v.spawn_stream = fr["draws_d"]
+            v.mt = None
+        self._frame_env, self._frame_data = v, fr
+        return fr
+
     def step(self, action):
         assert self.game is not None, "Game state is not initialized."
         venv = self._venv
+        torch = venv.torch
+        fr = self._frame()
+        o = fr["offs"]
+        p0 = 0
         if self.rng == "reference":
-            # stage the next draws the step can consume (<= one per cell per tensor)
-            venv.set_spawn_stream(speedups._buffer.peek(2 * venv.H * venv.W), 0)
-        obs, reward, done, info = venv.step(np.array([action], dtype=np.int32))
+            # stage the next draws the step can consume (<= one per cell per tensor);
+            # the buffer is addressed from the running stream position, so nothing on
+            # the device needs rewinding
+            p0 = self._stream_at
+            fr["draws_h"].numpy()[:] = speedups._buffer.peek(2 * venv.H * venv.W)
+            fr["draws_d"].copy_(fr["draws_h"], non_blocking=True)
+            venv._draw_base = p0
+        fr["act_h"][0] = int(action)
+        venv.actions_dev.copy_(fr["act_h"], non_blocking=True)
+        venv.step_async(venv.actions_dev)
+        torch.cat(fr["views"], out=fr["dev"])
+        fr["host"].copy_(fr["dev"], non_blocking=True)
+        torch.cuda.current_stream(venv.device).synchronize()
+        h = fr["host_np"]
+        reward = float(h[o[1]:o[2]].view(np.float64)[0])
+        flags = int(h[o[2]])
         if self.rng == "reference":
-            speedups._buffer.take(int(venv.stream_pos.item()))
-        reward = float(reward[0].item())
+            self._stream_at = int(h[o[3]:o[4]].view(np.int64)[0])
+            speedups._buffer.take(self._stream_at - p0)
+        obs = h[o[0]:o[1]].view(fr["obs_dtype"]).reshape(venv.obs.shape[1:]).copy()
+        H, W = venv.H, venv.W
+        board = h[o[4]:o[5]].view(np.uint16).reshape(H, W).copy()
+        goals = h[o[5]:o[6]].view(np.uint16).reshape(H, W).copy()
+        agent_loc = np.array([int(h[o[6]:o[7]].view(np.int32)[0]),
+                              int(h[o[7]:o[8]].view(np.int32)[0])])
         self.episode_length += 1
         self.episode_reward += reward
-        times_up = bool(info["times_up"][0].item())
+        times_up = bool(flags & 1)
         already_completed = self.episode_completed
-        self.episode_completed = times_up or bool(info["game_over"][0].item())
+        self.episode_completed = times_up or bool(flags & 2)
         if not already_completed and self.global_counter is not None:
             self.global_counter.episodes_completed += self.episode_completed
             self.global_counter.num_steps += 1
-        return obs[0].cpu().numpy(), reward, self.episode_completed, {
-            "board": self.game.board,
-            "goals": self.game.goals,
-            "agent_loc": self.game.agent_loc,
+        return obs, reward, self.episode_completed, {
+            "board": board,
+            "goals": goals,
+            "agent_loc": agent_loc,
             "times_up": times_up,
             "episode": {"length": self.episode_length, "reward": self.episode_reward},
         }

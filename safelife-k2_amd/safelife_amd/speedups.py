@@ -82,19 +82,68 @@ def _to_device_board(board, device):
     return torch.from_numpy(np.ascontiguousarray(a)).to(device), False
 
 
+class _Frames:
+    """Pinned host + device staging for one board shape: [board u16 | draws f64] up and
+    [new board u16 | draw count i64] down, so a numpy call is one copy each way and
+    one host sync (the board's draws are peeked -- at most one per cell -- and only the
+    count the device reports is then consumed)."""
+    _cache = {}
+
+    @classmethod
+    def get(cls, H, W, device):
+        key = (H, W, str(device))
+        if key not in cls._cache:
+            cls._cache[key] = cls(H, W, device)
+        return cls._cache[key]
+
+    def __init__(self, H, W, device):
+        import torch
+        n = H * W
+        self.nb = (2 * n + 7) // 8 * 8                  # board bytes, padded to 8
+        up, down = self.nb + 8 * n, self.nb + 8
+        self.up_h = torch.empty(up, dtype=torch.uint8, pin_memory=True)
+        self.up_d = torch.empty(up, dtype=torch.uint8, device=device)
+        self.dn_h = torch.empty(down, dtype=torch.uint8, pin_memory=True)
+        self.dn_d = torch.empty(down, dtype=torch.uint8, device=device)
+        self.off = torch.zeros(1, dtype=torch.int64, device=device)
+        self.up_np = self.up_h.numpy()
+        self.dn_np = self.dn_h.numpy()
+
+
 def advance_board(board, spawn_prob=0.3):
     """Advance one board; returns a new array (numpy in -> numpy out, torch -> torch)."""
     import torch
     device = _lib.require_device()
-    t, is_torch = _to_device_board(board, device)
+    p = float(np.float32(spawn_prob))
+    L = _lib.lib()
+    s = _lib.stream_ptr(device)
+    if not isinstance(board, torch.Tensor):
+        a = np.asarray(board)
+        if a.ndim != 2 or a.size == 0:
+            raise ValueError("advance_board expects a non-empty 2-d board")
+        H, W = a.shape
+        if H < 2 or W < 2:
+            raise ValueError("advance_board needs H, W >= 2")
+        f = _Frames.get(H, W, device)
+        n = H * W
+        f.up_np[:2 * n] = np.ascontiguousarray(a, dtype=np.uint16).reshape(-1).view(np.uint8)
+        f.up_np[f.nb:] = _buffer.peek(n).view(np.uint8)
+        f.up_d.copy_(f.up_h, non_blocking=True)
+        bd = f.up_d.data_ptr()
+        _lib.check(L.sl_count_eligible(bd, f.dn_d.data_ptr() + f.nb, 1, H, W, s),
+                   "sl_count_eligible")
+        _lib.check(L.sl_advance(bd, f.dn_d.data_ptr(), 1, H, W, None, p, _lib.SL_RNG_STREAM,
+                                0, 0, 0, 0, bd + f.nb, f.off.data_ptr(), s), "sl_advance")
+        f.dn_h.copy_(f.dn_d, non_blocking=True)
+        torch.cuda.current_stream(device).synchronize()
+        _buffer.take(int(f.dn_np[f.nb:].view(np.int64)[0]))   # consumed whatever p is
+        return f.dn_np[:2 * n].view(np.uint16).reshape(H, W).copy()
+    t, _ = _to_device_board(board, device)
     if t.dim() != 2 or t.numel() == 0:
         raise ValueError("advance_board expects a non-empty 2-d board")
     H, W = t.shape
     if H < 2 or W < 2:
         raise ValueError("advance_board needs H, W >= 2")
-    p = float(np.float32(spawn_prob))
-    L = _lib.lib()
-    s = _lib.stream_ptr(device)
     cnt = torch.zeros(1, dtype=torch.int64, device=device)
     _lib.check(L.sl_count_eligible(t.data_ptr(), cnt.data_ptr(), 1, H, W, s), "sl_count_eligible")
     n = int(cnt.item())
@@ -104,9 +153,7 @@ def advance_board(board, spawn_prob=0.3):
     out = torch.empty_like(t)
     _lib.check(L.sl_advance(t.data_ptr(), out.data_ptr(), 1, H, W, None, p, _lib.SL_RNG_STREAM,
                             0, 0, 0, 0, d.data_ptr(), off.data_ptr(), s), "sl_advance")
-    if is_torch:
-        return out
-    return out.cpu().numpy()
+    return out
 
 
 def advance_boards(boards, spawn_prob=0.3, rng="philox", seed=0, env0=0, step=0, tensor=0,

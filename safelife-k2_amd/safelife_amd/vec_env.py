@@ -16,9 +16,12 @@ the host only fills scalar arguments.  There is no CPU fallback.
 
 RNG: ``rng="philox"`` (default) draws each spawn uniform from Philox4x32-10 keyed by
 (seed; cell, global env id, step, tensor), so results do not depend on how the
-batch is sharded.  ``rng="stream"`` replays a supplied uniform stream in the
-reference's order (env by env, board then goals, row-major eligible cells), which
-is how the reference's global-numpy buffer (speedups_src/random.c) is matched.
+batch is sharded.  ``rng="stream"`` replays the reference's stream in the reference's
+order (env by env, board then goals, row-major eligible cells), which is how the
+reference's global-numpy buffer (speedups_src/random.c) is matched: either a supplied
+uniform buffer (``spawn_stream``), or, with ``spawn_stream=None``, the stream of
+``speedups.seed(seed)`` -- np.random.RandomState(seed).random_sample -- generated on the
+device inside each step (:class:`safelife_amd.mtstream.MT19937Stream`).
 """
 import ctypes
 import math
@@ -112,6 +115,7 @@ class SafeLifeVecEnv:
         self._abandoned = 0          # explicit resets of episodes that had not ended
         self._synced = (0, 0)        # (started, completed) already in global_counter
         self._recorder = None        # TrajectoryRecorder attached to this env
+        self._draw_base = 0          # stream position of spawn_stream[0]
         self._alloc(obs_dtype)
         # may any env's board or goals hold a spawning cell (bit 7)?  Spawners come only
         # from levels (no rule or action creates one) unless powers can be toggled; when
@@ -125,10 +129,19 @@ class SafeLifeVecEnv:
         if self.output_channels is not None and obs_dtype != "uint16":
             self.observation_space = Box(0, 1, self.observation_space.shape,
                                          np.uint8 if obs_dtype == "uint8" else np.float32)
+        self.mt = None
         if rng == "stream":
             if spawn_stream is None:
-                raise ValueError("rng='stream' needs spawn_stream (uniform doubles)")
-            self.set_spawn_stream(spawn_stream)
+                # the reference's seeded stream, generated on the device: the ring holds
+                # a quarter of a cell per env (C5's steady state draws 1/12), and one
+                # fill can generate a whole ring
+                self.spawn_stream = None
+                from .mtstream import MT19937Stream
+                self.mt = MT19937Stream(self.seed, self.device,
+                                        ring_draws=max(1 << 22, self.n_total_envs * self.H *
+                                                       self.W // 4))
+            else:
+                self.set_spawn_stream(spawn_stream)
         elif rng != "philox":
             raise ValueError("rng must be 'philox' or 'stream'")
         self._bonus_key = None
@@ -227,7 +240,15 @@ class SafeLifeVecEnv:
         else:
             s = torch.as_tensor(np.ascontiguousarray(stream, dtype=np.float64)).to(self.device)
         self.spawn_stream = s
+        self.mt = None
+        self._draw_base = 0
         self.stream_pos.fill_(int(pos))
+
+    def seek_stream(self, pos):
+        """Move the replay stream to draw `pos` (the device generator re-seeds there)."""
+        self.stream_pos.fill_(int(pos))
+        if self.mt is not None:
+            self.mt.seek(int(pos))
 
     def _bonus_table(self):
         key = (self.movement_bonus, self.movement_bonus_power, self.movement_bonus_period)
@@ -264,9 +285,16 @@ class SafeLifeVecEnv:
         c.seed = self.seed & 0xFFFFFFFFFFFFFFFF
         c.step = self._step_index & 0xFFFFFFFF
         c.env0 = self.env0
-        if self.rng == "stream":
-            c.draws = self.spawn_stream.data_ptr()
-            c.n_draws = self.spawn_stream.numel()
+        c.mt = None
+        if self.rng == "stream" and self.mt is not None:
+            c.draws = None
+            c.n_draws = 0
+            c.mt = ctypes.addressof(self.mt.struct)
+        elif self.rng == "stream":
+            # _draw_base: the supplied buffer starts at this stream position (a window
+            # of the stream staged per step by the single-env drop-in)
+            c.draws = self.spawn_stream.data_ptr() - 8 * self._draw_base
+            c.n_draws = self.spawn_stream.numel() + self._draw_base
         else:
             c.draws = None
             c.n_draws = 0
@@ -472,7 +500,8 @@ class SafeLifeVecEnv:
         return self.st_t
 
     def stream_error(self):
-        """True if rng='stream' ran past the end of the supplied stream."""
+        """True if rng='stream' ran past the end of the supplied stream (or asked the
+        device generator for a range it could not serve)."""
         return bool(self.scratch[8 * self.B].item() & 1)
 
     def set_state(self, board, goals, start_board, **scalars):
@@ -525,4 +554,6 @@ class SafeLifeVecEnv:
             v.copy_(d[k])
         self._step_index = int(d["step_index"])
         self.stream_pos.copy_(d["stream_pos"])
+        if self.mt is not None:
+            self.mt.seek(int(self.stream_pos.item()))
         self._invalidate_caches()

@@ -77,3 +77,34 @@ def test_build_id_file_matches_library():
     bid = bench.file_build_id()
     assert bid and len(bid) == 16
     assert _lib.build_id() == bid
+
+
+def test_cache_resident_configs_claim_no_hbm_fraction():
+    """C2 (4 096 x 25x25, ~15 MB of state) stays in the Infinity Cache: bench.py prints
+    roofline.bound "cache" with no frac and times its kernel over one bracket of all
+    timed steps (so kernel_ms <= ms_per_step); the HBM configs keep "hbm"."""
+    assert bench.roofline_bound(25, 25, 4096) == "cache"
+    assert bench.roofline_bound(64, 64, 65536) == "hbm"
+    assert bench.roofline_bound(64, 64, 32768) == "hbm"          # C4's shard
+    assert bench.roofline_bound(128, 128, 65536) == "hbm"
+    assert bench.state_bytes(25, 25, 4096) < bench.CACHE_RESIDENT_BYTES
+
+
+def test_seeded_replay_names():
+    """--rng seeded runs the replay kernels with the device generator; its PMC record
+    is its own."""
+    assert bench.step_kernel_name(128, 128, "none", "auto", "seeded") == "k_env_step_bits128<3>"
+    assert bench.pmc_record_path("c5", "none", "seeded").endswith("pmc_c5_seeded.json")
+    assert bench.pmc_record_path("c5", "none", "stream").endswith("pmc_c5_stream.json")
+
+
+def test_c1_cpu_leg_single_level():
+    """C1's CPU chain leg takes the single 25x25 level file (one env, one thread)."""
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--cpu-leg", json.dumps(
+        {"pools": [os.path.join(REPO, "tests", "golden", "levels", bench.C1_LEVEL)],
+         "threads": 1, "envs": 1, "seconds": 0.3,
+         "kw": {"time_limit": 1000, "view_shape": [33, 33], "penalty_coef": 1.0,
+                "min_performance": 0.01}})], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["n"] > 0 and r["rate"] > 0

@@ -45,7 +45,7 @@ def test_struct_layout_matches_header(tmp_path):
     from safelife_amd import _lib
     prog = tmp_path / "layout.c"
     fields = {"sl_env_state": _lib.EnvState, "sl_level_pool": _lib.LevelPool,
-              "sl_env_cfg": _lib.EnvCfg, "sl_capture": _lib.Capture}
+              "sl_env_cfg": _lib.EnvCfg, "sl_capture": _lib.Capture, "sl_mt19937": _lib.MT19937}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s"' % HEADER,
              'int main(void){']
     for cname, cls in fields.items():

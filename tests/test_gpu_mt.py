@@ -1,0 +1,225 @@
+"""The reference's seeded spawn stream generated on the device (csrc/sl_mt.hip,
+safelife_amd.mtstream), against numpy's RandomState itself.
+
+After speedups.seed(s) the reference draws every spawn uniform from numpy's global
+RandomState(s) (speedups_src/random.c:14-52, module.c:246-253): the stream is
+np.random.RandomState(s).random_sample.  Checked here:
+  * the ring against numpy over consecutive fills of step-like sizes, and after seeks
+    far into the stream (there against the host jump, itself checked against numpy in
+    tests/test_mt_cpu.py);
+  * G2 (tests/golden/advance_stream.npz, captured from the reference) and the golden
+    trajectories replayed from their seed alone -- no host stream;
+  * C5 at full batch (65 536 x 128x128, bench.py's regime, no rewind): the sampled envs'
+    slices of the generated stream are numpy's own draws at the device's offsets, and
+    the oracle fed those draws stays bit-exact.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from test_gpu_bench_regime import (CONFIGS, KW, POOLS, SEED, _OffsetStream, _oracle_levels,
+                                   _sample)
+from test_gpu_headline import _env_state, torch_dev  # noqa: F401
+from test_gpu_parity import _traj_files, _vec_env_from_traj
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+pytestmark = pytest.mark.gpu
+
+
+def _ring_slice(torch, mt, lo, hi):
+    idx = torch.arange(int(lo), int(hi), device=mt.device) & mt.mask
+    return mt.ring[idx].cpu().numpy()
+
+
+@pytest.mark.parametrize("rounds,n_chains,ring", [(33, 16, 1 << 21), (420, 64, 1 << 24)])
+def test_fill_matches_numpy(torch_dev, rounds, n_chains, ring):
+    """Consecutive ranges, as replay steps consume the stream: empty, single draws,
+    block-sized and multi-block ranges, all equal to RandomState(s).random_sample."""
+    torch, dev = torch_dev
+    from safelife_amd.mtstream import MT19937Stream
+    mt = MT19937Stream(2024, dev, ring_draws=ring, n_chains=n_chains, rounds=rounds)
+    D = mt.block
+    ref = np.random.RandomState(2024).random_sample(6 * n_chains * D)
+    rng = np.random.RandomState(0)
+    lohi = torch.zeros(2, dtype=torch.int64, device=dev)
+    pos, n_fills = 0, 0
+    sizes = [0, 1, 7, D - 1, D, D + 1, 3 * D + 17, (n_chains - 2) * D]
+    while pos + (n_chains - 1) * D < len(ref):
+        n = int(sizes[rng.randint(len(sizes))])
+        lohi[0], lohi[1] = pos, pos + n
+        mt.fill(lohi[0:1], lohi[1:2])
+        assert np.array_equal(_ring_slice(torch, mt, pos, pos + n), ref[pos:pos + n]), (pos, n)
+        pos += n
+        n_fills += 1
+    assert n_fills > 10 and not mt.error()
+
+
+def test_seek_far_into_the_stream(torch_dev):
+    from safelife_amd.mtstream import MT19937Stream, host_window, host_jump, host_jump_poly, \
+        host_draws
+    torch, dev = torch_dev
+    mt = MT19937Stream(77, dev, ring_draws=1 << 22, n_chains=32)
+    near = 7_777_777
+    mt.seek(near)
+    got = mt.draws(near, 250_000).cpu().numpy()
+    assert np.array_equal(got, np.random.RandomState(77).random_sample(near + 250_000)[near:])
+    for far in (3 * 10 ** 9 + 12345, (1 << 36) + 3):
+        mt.seek(far)
+        ref = host_draws(host_jump(host_window(77), host_jump_poly(2 * far)), 200_000)
+        assert np.array_equal(mt.draws(far, 200_000).cpu().numpy(), ref), far
+    # a rewound position is refused (flagged), not silently served stale
+    lohi = torch.tensor([0, 10], dtype=torch.int64, device=dev)
+    mt.fill(lohi[0:1], lohi[1:2])
+    assert mt.error()
+
+
+def test_g2_reproduced_from_seed_alone(torch_dev):
+    """G2 (spawner boards advanced 50 times after speedups.seed(s), captured from the
+    reference): the same boards from the device generator seeded with s, each
+    advance taking its draws at the running stream position (board, then goals)."""
+    torch, dev = torch_dev
+    from safelife_amd import speedups
+    from safelife_amd.mtstream import MT19937Stream
+    d = np.load(os.path.join(GOLDEN, "advance_stream.npz"))
+    keys = sorted({k.rsplit("_", 1)[0] for k in d.files if k.endswith("_board0")})
+    assert len(keys) >= 12
+    n_draws = 0
+    for key in keys:
+        s = int(key.split("_")[0][1:])
+        mt = MT19937Stream(s, dev, ring_draws=1 << 20, n_chains=4, rounds=33)
+        bg = torch.from_numpy(np.stack([d[key + "_board0"], d[key + "_goals0"]])).to(dev)
+        pos = 0
+        for t in range(d[key + "_boards"].shape[0]):
+            nb, ng = (int(c) for c in speedups.count_eligible(bg).cpu().numpy())
+            draws = mt.draws(pos, nb + ng)
+            offs = torch.tensor([0, nb], dtype=torch.int64, device=dev)
+            bg = speedups.advance_boards(bg, 0.3, rng="stream", draws=draws, draw_offsets=offs)
+            pos += nb + ng
+            out = bg.cpu().numpy()
+            assert np.array_equal(out[0], d[key + "_boards"][t]), (key, t)
+            assert np.array_equal(out[1], d[key + "_goals"][t]), (key, t)
+        n_draws += pos
+    assert n_draws > 0
+
+
+@pytest.mark.parametrize("path", _traj_files(), ids=lambda p: os.path.basename(p)[5:-4])
+def test_golden_trajectory_from_seed_alone(torch_dev, path):
+    """The reference-captured PPO-chain trajectories (speedups.seed(cfg seed), then
+    1 100 env steps) through the bit-sliced kernels with the spawn stream generated on
+    the device inside each step: boards, goals, rewards, views bit-exact."""
+    torch, dev = torch_dev
+    d = np.load(path)
+    seed = int(d["cfg"][2])
+    env = _vec_env_from_traj(d, kernel="fast", spawn_stream=None, seed=seed)
+    assert env.mt is not None
+    obs = env.reset().cpu().numpy()
+    assert np.array_equal(obs[0], d["obs0"])
+    actions = torch.from_numpy(d["action"].astype(np.int32)).to(dev)
+    for t in range(len(d["action"])):
+        obs, r, done, info = env.step(actions[t:t + 1])
+        ctx = (os.path.basename(path), t)
+        assert r.item() == d["reward"][t], ctx
+        assert bool(done.item()) == bool(d["done"][t]), ctx
+        assert np.array_equal(env.board[0].cpu().numpy(), d["board"][t]), ctx
+        assert np.array_equal(env.goals[0].cpu().numpy(), d["goals"][t]), ctx
+        assert np.array_equal(obs[0].cpu().numpy(), d["obs"][t]), ctx
+    assert not env.stream_error()
+
+
+class _NumpyStream:
+    """RandomState(seed).random_sample, extended on demand (slices as torch tensors)."""
+
+    def __init__(self, torch, seed):
+        self.torch, self.rs, self.a = torch, np.random.RandomState(seed), np.zeros(0)
+
+    def __getitem__(self, sl):
+        if sl.stop > len(self.a):
+            self.a = np.concatenate([self.a, self.rs.random_sample(sl.stop - len(self.a))])
+        return self.torch.from_numpy(self.a[sl])
+
+
+class _RingStream:
+    def __init__(self, torch, mt):
+        self.torch, self.mt = torch, mt
+
+    def __getitem__(self, sl):
+        return self.torch.from_numpy(_ring_slice(self.torch, self.mt, sl.start, sl.stop))
+
+
+def _seeded_steps(torch, dev, venv, oenvs, ostreams, sample, T, rng):
+    B = venv.B
+    n_reset = 0
+    for t in range(T):
+        acts = rng.randint(0, 9, size=B).astype(np.int32)
+        _, vr, vd, info = venv.step(torch.from_numpy(acts).to(dev))
+        rs = info["reset"].cpu().numpy()
+        vr, vd = vr.cpu().numpy(), vd.cpu().numpy()
+        offs = venv.scratch[2 * B:4 * B].cpu().numpy()
+        end = int(venv.stream_pos.item())
+        nxt = lambda k: int(offs[k]) if k < 2 * B else end          # noqa: E731
+        for e in sample:
+            ostreams[e].arm(int(offs[2 * e]), int(offs[2 * e + 1]), nxt(2 * e + 2))
+        for e in sample:
+            _, r, dn, _ = oenvs[e].step(int(acts[e]))
+            n_reset += int(rs[e])
+            assert vr[e] == r, (t, e)
+            assert bool(vd[e]) == dn, (t, e)
+            assert np.array_equal(venv.board[e].cpu().numpy(), oenvs[e].board), (t, e)
+            assert np.array_equal(venv.goals[e].cpu().numpy(), oenvs[e].goals), (t, e)
+            assert not ostreams[e].bounds, (t, e)
+    return n_reset
+
+
+def test_seeded_replay_c5_full_batch_vs_numpy(torch_dev):
+    """C5 at full batch with the stream generated on the device (what bench.py
+    --rng seeded times; no rewind, no host buffer): for the first steps the sampled
+    envs' oracles draw from numpy's own RandomState(SEED).random_sample at the device's
+    offsets; after 120 more steps (positions ~10^10) from the ring, whose slices are
+    then checked against the host jump at the sampled offsets."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    from safelife_amd.mtstream import host_window, host_jump, host_jump_poly, host_draws
+    fname, B = CONFIGS["c5"]
+    pool = LevelPool.load(os.path.join(POOLS, fname))
+    venv = SafeLifeVecEnv(pool, B, dev, rng="stream", spawn_stream=None, seed=SEED,
+                          level_order="random", augment_roll=True, kernel="fast",
+                          compute_obs=False, **KW)
+    venv.reset()
+    g = torch.Generator(device=dev)
+    g.manual_seed(99)
+    venv.st_t["episode_length"].copy_(torch.randint(0, KW["time_limit"], (B,), device=dev,
+                                                    generator=g, dtype=torch.int32))
+    levels = _oracle_levels(pool)
+
+    def oracles(stream):
+        sample = _sample(venv)
+        oenvs, ostreams = {}, {}
+        for e in sample:
+            ostreams[e] = _OffsetStream(stream)
+            o = oracle.OracleEnv(oracle.pool_level_fn(levels, e, seed=SEED, random_order=True,
+                                                      augment=True),
+                                 env_id=e, rng="stream", seed=SEED, stream=ostreams[e], **KW)
+            o.load_state(_env_state(venv, e), venv._step_index)
+            oenvs[e] = o
+        return sample, oenvs, ostreams
+
+    rng = np.random.RandomState(6)
+    sample, oenvs, ostreams = oracles(_NumpyStream(torch, SEED))
+    _seeded_steps(torch, dev, venv, oenvs, ostreams, sample, 2, rng)
+    for _ in range(120):
+        venv.step_async(torch.randint(0, 9, (B,), dtype=torch.int32, device=dev, generator=g))
+    pos0 = int(venv.stream_pos.item())
+    assert pos0 > 10 ** 9
+    sample, oenvs, ostreams = oracles(_RingStream(torch, venv.mt))
+    n_reset = _seeded_steps(torch, dev, venv, oenvs, ostreams, sample, 1, rng)
+    # the ring's slices of that step are numpy's stream (host jump from the seed)
+    offs = venv.scratch[2 * B:4 * B].cpu().numpy()
+    for e in sample[:4]:
+        lo = int(offs[2 * e])
+        ref = host_draws(host_jump(host_window(SEED), host_jump_poly(2 * lo)), 4000)
+        assert np.array_equal(_ring_slice(torch, venv.mt, lo, lo + 4000), ref), e
+    n_reset += _seeded_steps(torch, dev, venv, oenvs, ostreams, sample, 30, rng)
+    assert n_reset >= 6
+    assert not venv.stream_error()
