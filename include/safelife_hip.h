@@ -134,9 +134,9 @@ int sl_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n,
  *   chains   uint32 [n_chains, 624]          the MT state of each chain's next block
  *   prefix   uint32 [n_chains, SL_MT_PREFIX] scratch
  *   polys    uint32 [log2(n_chains) + 1, SL_MT_POLY_WORDS] jump polynomials
- *   ctl      int64 [4]: next block to generate, a done counter, error flags (bit0:
+ *   ctl      int64 [6]: next block to generate, a done counter, error flags (bit0:
  *            a fill asked for a range the ring or the chains cannot serve), the
- *            first block
+ *            first block, the next block whose chain has to jump, a done counter
  * n_chains is a power of two (one fill generates at most n_chains blocks), rounds
  * >= 33, ring_draws a power of two >= 2 blocks.
  */

@@ -348,6 +348,8 @@ __device__ __forceinline__ int lds_cell_idx(int row, int col) {
     return row * 64 + ((col + 32 * (row >> 5)) & 63);
 }
 
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+
 // exit y (R_EY) or x (R_EX) number e of the record, e = this lane's own index
 __device__ __forceinline__ int lane_exit(const RecFields &fl, int e, int field) {
     const u32 w = (u32)__builtin_amdgcn_ds_bpermute(4 * (field + (e >> 1)), (int)fl.V);
@@ -356,7 +358,6 @@ __device__ __forceinline__ int lane_exit(const RecFields &fl, int e, int field) 
 
 __device__ __forceinline__ void write_obs(lds_u32 *buf, const FastExtra &fx, const RecFields &fl,
                                           int64_t b, int lane) {
-    typedef __attribute__((address_space(3))) uint16_t lds_u16;
     lds_u16 *cells = reinterpret_cast<lds_u16 *>(buf);
     (void)fx;
     const FastExtra &lfx = kernarg().fx;     // read late: no SGPRs held through the step
@@ -414,6 +415,57 @@ __device__ __forceinline__ void write_obs(lds_u32 *buf, const FastExtra &fx, con
     }
 }
 
+// Fused channel views (output_channels = a channel list: the reference's default
+// 15 channels, safelife_env.py:79,150-154) of the view-form board in LDS (the same
+// board write_obs reads, exits moved in place; views no larger than the board): each
+// view cell's channel mask goes to the wave's mask array, then the env's output
+// bytes leave as 16-byte chunks (obs_store_channels, sl_obs.h) -- no re-read of the
+// state from HBM as the separate k_env_obs_channels needs.
+template <int ESZ>
+__device__ __forceinline__ void write_obs_channels(lds_u32 *buf, uint16_t *vm, const RecFields &fl,
+                                                   int64_t b, int lane) {
+    lds_u16 *cells = reinterpret_cast<lds_u16 *>(buf);
+    const FastExtra &lfx = kernarg().fx;     // read late: no SGPRs held through the step
+    const int vh = lfx.obs_vh, vw = lfx.obs_vw;
+    const int nv = vh * vw;
+    const int ty = fl.ay - vh / 2, tx = fl.ax - vw / 2;
+    const int ne = min(fl.exit_count(), SL_MAX_EXITS);
+    int tgt = -1;
+    u32 val = 0u;
+    const int iy = lane_exit(fl, lane & 7, R_EY), ix = lane_exit(fl, lane & 7, R_EX);
+    if (lane < ne) {
+        int jy = ((iy - fl.ay + N / 2) & (N - 1)) - N / 2;
+        int jx = ((ix - fl.ax + N / 2) & (N - 1)) - N / 2;
+        jy = min(max(jy + vh / 2, 0), vh - 1);
+        jx = min(max(jx + vw / 2, 0), vw - 1);
+        val = cells[lds_cell_idx(iy, ix)];
+        tgt = lds_cell_idx((ty + jy) & (N - 1), (tx + jx) & (N - 1));
+    }
+    for (int k = 0; k < ne; k++)              // in np.nonzero order: the last one wins
+        if (lane == k) cells[tgt] = (uint16_t)val;
+    const sl::obs::ChanMap cm{lfx.obs_chpack, lfx.obs_nch};
+    const bool id = cm.ident();
+    const int dr = 64 / vw, dc = 64 - dr * vw;
+    int r = lane / vw, c = lane - r * vw;
+    for (int i = lane; i < nv; i += 64) {
+        vm[i] = (uint16_t)cm.mask(cells[lds_cell_idx((ty + r) & (N - 1), (tx + c) & (N - 1))], id);
+        r += dr;
+        c += dc;
+        if (c >= vw) {
+            c -= vw;
+            r++;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    sl::obs::obs_store_channels<ESZ>(vm, nv, cm.nch, lfx.obs_one, b, lane,
+                                     reinterpret_cast<uint8_t *>(lfx.obs_out));
+}
+
+// the instantiations' view modes: 0 none, 1 packed, 2 channels of 2-byte elements (u16,
+// bf16), 3 of 1-byte (u8), 4 of 4-byte (f32)
+constexpr int obs_esz(int OBS) { return OBS == 3 ? 1 : (OBS == 4 ? 4 : 2); }
+
 // What an env's step needs first, issued ahead: the per-env record (lane k = field k)
 // and the goals' three colour planes from the mirror (speculative: used when the
 // mirror is valid).  The board itself is DMA'd into the wave's LDS buffer.
@@ -439,13 +491,14 @@ __device__ __forceinline__ void issue_pre(const sl_env_state &st, const int32_t 
 // is in flight into `buf` (issued by the caller).  MODE: SPAWN_PHILOX, or SPAWN_STREAM
 // (replay: k_env_action has run the action and k_stream_prologue64 sized the draws; the step reads
 // act[b] and each tensor's first uniform from the scratch words).
-template <bool OBS, int MODE>
+template <int OBS, int MODE>
 __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs &a,
                                          const FastExtra &fx, int64_t b, int lane, lds_u32 *buf,
-                                         const int32_t *__restrict__ actions, int ctp, int ctc,
-                                         double *reward_out, uint8_t *done_out,
+                                         uint16_t *vm, const int32_t *__restrict__ actions,
+                                         int ctp, int ctc, double *reward_out, uint8_t *done_out,
                                          uint8_t *flags_out, int32_t *ep_len_out,
                                          int32_t *ep_rew_out, const Pre &pre) {
+    constexpr bool VIEW = OBS != 0, CH = OBS >= 2;
     const int64_t off = b * (int64_t)(N * N);
     const int lane_off = (lane & 1) * 1024 + (lane >> 1);     // dwords: row 32h, column pair j
     u32 *gb = reinterpret_cast<u32 *>(st.board + off) + lane_off;
@@ -573,9 +626,9 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     // check) the goal colours go into planes 12-14 now -- the scores read them there
     // and the goal planes die before the scoring -- and ONE transpose later yields
     // both the board rows and the view rows
-    const bool hi = OBS && __ballot((PL(PB, 12, 0) | PL(PB, 13, 0) | PL(PB, 14, 0) |
-                                     PL(PB, 12, 1) | PL(PB, 13, 1) | PL(PB, 14, 1)) != 0u) != 0ull;
-    if (OBS && !hi) {
+    const bool hi = VIEW && __ballot((PL(PB, 12, 0) | PL(PB, 13, 0) | PL(PB, 14, 0) |
+                                      PL(PB, 12, 1) | PL(PB, 13, 1) | PL(PB, 14, 1)) != 0u) != 0ull;
+    if (VIEW && !hi) {
         const int obs_rw = kernarg().fx.obs_rw;
 #pragma unroll
         for (int w = 0; w < 2; w++) {
@@ -595,7 +648,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         transpose32(PS);
     }
     int pts, scr, pos, side;
-    if (OBS && !hi) score_planes<true>(PB, gcol, PS, &pts, &scr, &pos, &side);
+    if (VIEW && !hi) score_planes<true>(PB, gcol, PS, &pts, &scr, &pos, &side);
     else score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
     // totals (packed two per word: per-lane ranges [-192, 320] and [-64, 64]);
     // reduced before the board store so the scoring is not sunk past it
@@ -611,13 +664,13 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     const int possible = s2 & 0xFFFF;
     const int side_total = (s2 >> 16) & 0xFFFF;
     const u32 rb = wave_or(cb[0] | cb[1]) | erow;
-    if (rb || OBS) {
+    if (rb || VIEW) {
         const bool can = can_exit_now(fl.min_performance(), score, fl.baseline(), possible);
 #pragma unroll
         for (int w = 0; w < 2; w++)
             PL(PB, 9, w) = can ? (PL(PB, 9, w) | PL(PB, 8, w)) : (PL(PB, 9, w) & ~PL(PB, 8, w));
         transpose32(PB);
-        if (OBS && !hi) {
+        if (VIEW && !hi) {
             // planes 12-14 hold the goal colours: the store masks them out again
             if (rb) {
 #pragma unroll
@@ -631,9 +684,10 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
                 if ((rb >> y) & 1u) __builtin_nontemporal_store(PB[y], &gb[y * 32]);
         }
     }
-    if (OBS && !hi) {
+    if (VIEW && !hi) {
         __builtin_amdgcn_sched_barrier(0);
-        write_obs(buf, fx, fl, b, lane);
+        if (CH) write_obs_channels<obs_esz(OBS)>(buf, vm, fl, b, lane);
+        else write_obs(buf, fx, fl, b, lane);
         __builtin_amdgcn_sched_barrier(0);
     }
     int reset = 0;
@@ -641,7 +695,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         reset = epilogue_core(st, a, b, fl, act_reward, points, score, possible, side_total,
                               reward_out, done_out, flags_out, ep_len_out, ep_rew_out);
     reset = __builtin_amdgcn_readfirstlane(reset);
-    if (OBS && hi && !(fx.fuse_reset && reset)) {
+    if (VIEW && hi && !(fx.fuse_reset && reset)) {
         // a board using bits 12-14 (no cell type does): the view from the stored state
         // once everything has landed -- the action's writes, this step's goal and row
         // stores and the epilogue's exit cells (this wave's own stores) -- as
@@ -653,8 +707,14 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         oa.vh = lfx.obs_vh;
         oa.vw = lfx.obs_vw;
         oa.remove_white = lfx.obs_rw;
-        oa.mode = SL_OBS_PACKED;
-        sl::obs::obs_packed_wave(st, oa, b, lane, lfx.obs_out);
+        oa.mode = lfx.obs_mode;
+        oa.nch = lfx.obs_nch;
+        if (CH)
+            sl::obs::obs_channels_wave<obs_esz(OBS)>(
+                st, oa, sl::obs::ChanMap{lfx.obs_chpack, lfx.obs_nch}, lfx.obs_one, b, lane, vm,
+                reinterpret_cast<uint8_t *>(lfx.obs_out));
+        else
+            sl::obs::obs_packed_wave(st, oa, b, lane, lfx.obs_out);
     }
     if (fx.fuse_reset && reset && lane == 0) {
         // queue the env for the reset kernel (k_env_reset_list)
@@ -664,19 +724,23 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     }
 }
 
-// OBS: also write the packed observation (fx.obs_out); MODE: see step_env
-template <bool OBS, int MODE>
+// OBS: also write the observation (fx.obs_out): 1 packed, 2-4 channel views
+// (obs_esz); MODE: see step_env
+template <int OBS, int MODE>
 __global__ void __launch_bounds__(64, (OBS || MODE == SPAWN_STREAM) ? kMinWavesObs : kMinWaves)
 k_env_step_bits64(StepKArgs ka) {
     const int64_t b = blockIdx.x;          // one wave per env
     const int lane = threadIdx.x;
     __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
+    // channel views: the view's channel masks (write_obs_channels)
+    __shared__ __attribute__((aligned(16))) uint16_t vmask[OBS >= 2 ? sl::obs::kFusedChanCells : 2];
     lds_u32 *buf = (lds_u32 *)&stage[0];
     Pre pre;
     issue_pre(ka.st, ka.actions, b, lane, pre);
     dma_board(ka.st.board + b * (int64_t)(N * N), buf, lane);
-    step_env<OBS, MODE>(ka.st, ka.a, ka.fx, b, lane, buf, ka.actions, ka.ctp, ka.ctc, ka.reward_out,
-                  ka.done_out, ka.flags_out, ka.ep_len_out, ka.ep_rew_out, pre);
+    step_env<OBS, MODE>(ka.st, ka.a, ka.fx, b, lane, buf, vmask, ka.actions, ka.ctp, ka.ctc,
+                        ka.reward_out, ka.done_out, ka.flags_out, ka.ep_len_out, ka.ep_rew_out,
+                        pre);
 }
 
 // Replay-mode count of env b (SL_RNG_STREAM), one wave, after k_env_action (one lane
@@ -737,7 +801,10 @@ k_stream_prologue64(StepKArgs ka) {
 // (the step kernel wrote the views of all other envs).
 __global__ void __launch_bounds__(64)
 k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scratch,
-                 uint32_t step, sl::obs::ObsArgs oa, uint16_t *obs_out) {
+                 uint32_t step, sl::obs::ObsArgs oa, uint64_t chpack, uint32_t one,
+                 uint16_t *obs_out) {
+    // channel views of the reset envs: their masks
+    __shared__ __attribute__((aligned(16))) uint16_t vmask[sl::obs::kFusedChanCells];
     int64_t *cnt = scratch + 8 * st.B + 2;
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(step + 1) & 1] = 0;
     const int32_t *list = reset_list(scratch);
@@ -751,8 +818,39 @@ k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scr
         if (obs_out) {
             wait_vm();      // the reset's stores have landed (no stale lines: this wave
                             // alone touches env b, and L1 starts clean each launch)
-            sl::obs::obs_packed_wave(st, oa, b, threadIdx.x, obs_out);
+            const sl::obs::ChanMap cm{chpack, oa.nch};
+            uint8_t *o8 = reinterpret_cast<uint8_t *>(obs_out);
+            if (oa.mode == SL_OBS_PACKED)
+                sl::obs::obs_packed_wave(st, oa, b, threadIdx.x, obs_out);
+            else if (oa.mode == SL_OBS_CHANNELS_U8)
+                sl::obs::obs_channels_wave<1>(st, oa, cm, one, b, threadIdx.x, vmask, o8);
+            else if (oa.mode == SL_OBS_CHANNELS_F32)
+                sl::obs::obs_channels_wave<4>(st, oa, cm, one, b, threadIdx.x, vmask, o8);
+            else
+                sl::obs::obs_channels_wave<2>(st, oa, cm, one, b, threadIdx.x, vmask, o8);
         }
+    }
+}
+
+// the step kernel's view mode for fx (k_env_step_bits64's OBS)
+int obs_kind(const FastExtra &fx) {
+    if (!fx.obs_out) return 0;
+    switch (fx.obs_mode) {
+    case SL_OBS_PACKED: return 1;
+    case SL_OBS_CHANNELS_U8: return 3;
+    case SL_OBS_CHANNELS_F32: return 4;
+    default: return 2;               // u16 and bf16 channels
+    }
+}
+
+template <int MODE>
+void launch_bits64(int kind, unsigned grid, const StepKArgs &ka, hipStream_t s) {
+    switch (kind) {
+    case 0: hipLaunchKernelGGL((k_env_step_bits64<0, MODE>), dim3(grid), dim3(64), 0, s, ka); break;
+    case 1: hipLaunchKernelGGL((k_env_step_bits64<1, MODE>), dim3(grid), dim3(64), 0, s, ka); break;
+    case 2: hipLaunchKernelGGL((k_env_step_bits64<2, MODE>), dim3(grid), dim3(64), 0, s, ka); break;
+    case 3: hipLaunchKernelGGL((k_env_step_bits64<3, MODE>), dim3(grid), dim3(64), 0, s, ka); break;
+    default: hipLaunchKernelGGL((k_env_step_bits64<4, MODE>), dim3(grid), dim3(64), 0, s, ka); break;
     }
 }
 
@@ -778,16 +876,10 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         const int rc = stream_offsets(st, fx, s);
         if (rc || !stream_steps(fx)) return rc;
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        if (fx.obs_out)
-            hipLaunchKernelGGL((k_env_step_bits64<true, SPAWN_STREAM>), dim3(grid), dim3(64), 0, s, ka);
-        else
-            hipLaunchKernelGGL((k_env_step_bits64<false, SPAWN_STREAM>), dim3(grid), dim3(64), 0, s, ka);
+        launch_bits64<SPAWN_STREAM>(obs_kind(fx), grid, ka, s);
     } else {
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        if (fx.obs_out)
-            hipLaunchKernelGGL((k_env_step_bits64<true, SPAWN_PHILOX>), dim3(grid), dim3(64), 0, s, ka);
-        else
-            hipLaunchKernelGGL((k_env_step_bits64<false, SPAWN_PHILOX>), dim3(grid), dim3(64), 0, s, ka);
+        launch_bits64<SPAWN_PHILOX>(obs_kind(fx), grid, ka, s);
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);
@@ -801,10 +893,10 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         oa.vh = fx.obs_vh;
         oa.vw = fx.obs_vw;
         oa.remove_white = fx.obs_rw;
-        oa.mode = SL_OBS_PACKED;
-        oa.nch = 0;
+        oa.mode = fx.obs_mode;
+        oa.nch = fx.obs_nch;
         hipLaunchKernelGGL(k_env_reset_list, dim3(grid), dim3(64), 0, s, st, fx.pool, fx.ra,
-                           fx.scratch, a.step, oa, fx.obs_out);
+                           fx.scratch, a.step, oa, fx.obs_chpack, fx.obs_one, fx.obs_out);
     }
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }

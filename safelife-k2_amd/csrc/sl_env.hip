@@ -834,79 +834,9 @@ k_env_obs_channels(sl_env_state st, ObsArgs a, uint64_t chpack, uint32_t one, in
     extern __shared__ __attribute__((aligned(16))) uint16_t obs_lds[];
     const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int64_t b = (int64_t)blockIdx.x * 4 + wid;
-    const int lane = threadIdx.x & 63;
     if (b >= st.B) return;
-    ObsWave w;
-    obs_wave_init(st, a, b, w);
-    const int nv = a.vh * a.vw, nch = a.nch;
-    uint16_t *vw_ = obs_lds + wid * vpad;
-    // channels 0..nch-1 in order: the mask is the value's low bits
-    bool ident = true;
-    for (int k = 0; k < nch; k++) ident = ident && ((chpack >> (4 * k)) & 15u) == (uint64_t)k;
-    const uint32_t lowmask = (1u << nch) - 1u;
-    int i0 = lane, r = lane / a.vw, c = lane - (lane / a.vw) * a.vw;
-    while (i0 < nv)
-        obs_wave_cells(st, a, w, nv, i0, r, c, [&](int i, uint32_t v) {
-            uint32_t m = v & lowmask;
-            if (!ident) {
-                m = 0u;
-                for (int k = 0; k < nch; k++) m |= ((v >> ((chpack >> (4 * k)) & 15u)) & 1u) << k;
-            }
-            vw_[i] = (uint16_t)m;
-        });
-    // LDS operations of one wave complete in order: the reads below see the writes
-    __builtin_amdgcn_wave_barrier();
-    const int64_t n_el = (int64_t)nv * nch;                  // elements per env
-    const int64_t base = b * n_el * ESZ;                      // first byte
-    const int64_t end = base + n_el * ESZ;
-    const int64_t c0 = (base + 15) & ~(int64_t)15, c1 = end & ~(int64_t)15;
-    // partial chunks at both ends (< 16 bytes each): one element per lane
-    const int head = (int)(((c0 < end ? c0 : end) - base) / ESZ);
-    const int tail = c1 >= c0 ? (int)((end - c1) / ESZ) : 0;
-    int e = -1;                                               // elements per env < 2^16
-    if (lane < head) e = lane;
-    else if (lane >= 32 && lane - 32 < tail) e = (int)((c1 - base) / ESZ) + (lane - 32);
-    if (e >= 0) {
-        const int cell = e / nch, k = e - cell * nch;
-        const uint32_t v = ((vw_[cell] >> k) & 1u) ? one : 0u;
-        for (int t = 0; t < ESZ; t++) out[base + e * ESZ + t] = (uint8_t)(v >> (8 * t));
-    }
-    // whole chunks; a lane's next chunk starts 1024 / ESZ elements on, i.e. dcell
-    // cells and dk channels (no division in the loop)
-    constexpr int NE = 16 / ESZ, STEP = 1024 / ESZ;
-    const int dcell = STEP / nch, dk = STEP - dcell * nch;
-    int cell0, k0;
-    {
-        const int e0 = (int)((c0 - base) / ESZ) + lane * NE;
-        cell0 = e0 / nch;
-        k0 = e0 - cell0 * nch;
-    }
-    for (int64_t q = c0 + 16 * (int64_t)lane; q < c1; q += 16 * 64) {
-        // the chunk's NE element bits, low bit first
-        uint32_t bits = (uint32_t)vw_[cell0] >> k0;
-        int have = nch - k0, cn = cell0 + 1;
-        while (have < NE) {
-            bits |= (uint32_t)vw_[cn++] << have;
-            have += nch;
-        }
-        cell0 += dcell;
-        k0 += dk;
-        if (k0 >= nch) {
-            k0 -= nch;
-            cell0++;
-        }
-        uint32_t wv[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (ESZ == 1)        // 4 bits -> 4 bytes
-                wv[j] = ((((bits >> (4 * j)) & 15u) * 0x00204081u) & 0x01010101u) * one;
-            else if (ESZ == 2)   // 2 bits -> 2 halfwords
-                wv[j] = ((((bits >> (2 * j)) & 3u) * 0x8001u) & 0x00010001u) * one;
-            else                 // 1 bit -> 1 word
-                wv[j] = ((bits >> j) & 1u) * one;
-        }
-        *reinterpret_cast<uint4 *>(out + q) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-    }
+    obs_channels_wave<ESZ>(st, a, ChanMap{chpack, a.nch}, one, b, threadIdx.x & 63,
+                           obs_lds + wid * vpad, out);
 }
 
 bool set_lds(const void *fn, size_t bytes) {
@@ -1186,12 +1116,28 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
                                 cfg->obs_channels, cfg->obs_nch, &oa);
         if (rc) return rc;
     }
-    const bool fuse_obs = cfg->obs_out && fast && oa.mode == SL_OBS_PACKED &&
-                          oa.vh * oa.vw <= kObsMaxCells;
+    // ... and channel views too (one wave writes its env's 16-byte chunks from the
+    // view masks it builds in LDS: views up to kFusedChanCells cells, 16-B aligned out)
+    const bool fuse_obs =
+        cfg->obs_out && fast &&
+        ((oa.mode == SL_OBS_PACKED && oa.vh * oa.vw <= kObsMaxCells) ||
+         (oa.mode != SL_OBS_PACKED && oa.vh <= 64 && oa.vw <= 64 &&
+          oa.vh * oa.vw + 2 <= kFusedChanCells && (((uintptr_t)cfg->obs_out) & 15) == 0));
     fx.obs_out = fuse_obs ? (uint16_t *)cfg->obs_out : nullptr;
     fx.obs_vh = cfg->obs_vh;
     fx.obs_vw = cfg->obs_vw;
     fx.obs_rw = cfg->obs_remove_white;
+    fx.obs_mode = SL_OBS_PACKED;
+    fx.obs_nch = 0;
+    fx.obs_chpack = 0;
+    fx.obs_one = 1u;
+    if (cfg->obs_out) {
+        fx.obs_mode = oa.mode;
+        fx.obs_nch = oa.nch;
+        for (int k = 0; k < oa.nch; k++) fx.obs_chpack |= (uint64_t)oa.ch[k] << (4 * k);
+        fx.obs_one = oa.mode == SL_OBS_CHANNELS_F32 ? 0x3F800000u
+                     : oa.mode == SL_OBS_CHANNELS_BF16 ? 0x3F80u : 1u;
+    }
     if (fast128) {
         int rc = launch_step_bits128(*st, a, fx, actions, cfg->can_toggle_powers,
                                      cfg->can_toggle_colors, reward, done, info_flags, ep_len,

@@ -315,8 +315,12 @@ struct FastExtra {
     int64_t *scratch;       // sl_env_cfg.scratch (reset list + counters)
     void *ev_end;           // hipEvent_t recorded right after the step kernel's launch
                             // (before any follow-up kernel), or NULL
-    uint16_t *obs_out;      // 64x64 kernel: packed views written from the on-chip
-    int32_t obs_vh, obs_vw, obs_rw;   // board (NULL: none); view shape, remove_white
+    uint16_t *obs_out;      // 64x64 kernel: views written from the on-chip board (NULL:
+    int32_t obs_vh, obs_vw, obs_rw;   // none); view shape, remove_white
+    int32_t obs_mode;       // SL_OBS_PACKED or a channel mode (then obs_out is the
+    int32_t obs_nch;        // [B, vh, vw, nch] array of SL_OBS_CHANNELS*)
+    uint64_t obs_chpack;    // channel k in bits 4k .. 4k + 3
+    uint32_t obs_one;       // a channel element's 1 (1, 0x3F80 bf16, 0x3F800000 f32)
     const sl_capture *capture;        // trajectory capture (NULL: none): phase 0 is
                                       // launched between the step and reset kernels
     int32_t stream;         // SL_RNG_STREAM: replay prologue (action + eligible counts),

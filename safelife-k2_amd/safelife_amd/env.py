@@ -50,8 +50,11 @@ def _single_venv(level, device, rng="reference", seed=0, **kw):
                   global_counter=GlobalCounter())
     common.update(kw)
     if rng == "reference":
-        return SafeLifeVecEnv(pool, 1, device, rng="stream", spawn_stream=np.zeros(1), **common)
-    return SafeLifeVecEnv(pool, 1, device, rng="philox", seed=seed, **common)
+        v = SafeLifeVecEnv(pool, 1, device, rng="stream", spawn_stream=np.zeros(1), **common)
+    else:
+        v = SafeLifeVecEnv(pool, 1, device, rng="philox", seed=seed, **common)
+    v._dropin = True      # draws from the global speedups stream (rng='reference')
+    return v
 
 
 class SafeLifeGame:
@@ -81,6 +84,7 @@ class SafeLifeGame:
         self._pts = torch.zeros(1, dtype=torch.int32, device=venv.device)
         self._scratch = torch.zeros(8 + 16, dtype=torch.int64, device=venv.device)
         self._pos = torch.zeros(1, dtype=torch.int64, device=venv.device)
+        self._advances = 0           # Philox step counter of this game's own advances
 
     # ------------------------------------------------------------ construction
     @classmethod
@@ -129,6 +133,8 @@ class SafeLifeGame:
         self._venv.board[self._idx].copy_(self._upload(value))
         self._set("spawn_flags", self._st("spawn_flags") | 1)   # may now hold a spawner
         self._venv._may_spawn = True
+        # bit 3: the board's draw planes (128x128 replay) described the old board
+        self._venv.planes_ok[self._idx].bitwise_and_(~8)
         self.rescore()
 
     @property
@@ -367,21 +373,27 @@ class SafeLifeGame:
 
     def advance_board(self):
         """safelife_game.py:657-660 (num_steps += 1; board, then goals) on the
-        device.  Draws come from the global numpy stream (speedups) when the env
-        replays the reference stream, else from Philox at the env's next step
-        index."""
+        device.  Draws: the drop-in game (loaddata / SafeLifeEnv) replaying the
+        reference takes them from the global numpy stream (speedups); a view of a
+        batch with rng='stream' from the batch's own stream at its position (the
+        batch's replay order is its own business); Philox from this game's own
+        advance counter, which leaves the batch's step index -- and so every other
+        env's keys -- alone."""
         v = self._venv
         cfg = v._fill_cfg()
         cfg.scratch = self._scratch.data_ptr()
-        ref = v.rng == "stream"
+        ref = v.rng == "stream" and getattr(v, "_dropin", False)
         if ref:
             draws = v.torch.from_numpy(speedups._buffer.peek(2 * v.H * v.W)).to(v.device)
             self._pos.zero_()
             cfg.draws, cfg.n_draws, cfg.stream_pos = draws.data_ptr(), draws.numel(), \
                 self._pos.data_ptr()
-        else:
+            cfg.mt = None
+        elif v.rng != "stream":
             cfg.env0 = v.env0 + self._idx
-            v._step_index += 1
+            # (the top bit keeps these counters apart from the batch's step indices)
+            cfg.step = (0x80000000 | self._advances) & 0xFFFFFFFF
+            self._advances += 1
         _lib.check(_lib.lib().sl_env_advance(ctypes.byref(self._slice()), ctypes.byref(cfg),
                                              self._stream()), "sl_env_advance")
         if ref:
@@ -454,6 +466,17 @@ class SafeLifeGame:
         data = self.serialize()
         self._init = dict(data)
         self.num_steps = 0
+        # _init_data is now the saved state (safelife_game.py:225): performance_ratio,
+        # can_exit and the exit colours score against it, and the side-effect start
+        # board is it
+        v, i = self._venv, self._idx
+        self.rescore()
+        v.state["baseline"][i] = v.state["score"][i]
+        v.start_board[i].copy_(v.board[i])
+        v.state["start_roll"][i] = -1
+        hi = 4 if ((v.H, v.W) == (128, 128)
+                   and bool(start_board_hi_bits(v.start_board[i:i + 1])[0])) else 0
+        self._set("spawn_flags", (self._st("spawn_flags") & ~4) | hi)
         np.savez_compressed(file_name, **data)
 
 

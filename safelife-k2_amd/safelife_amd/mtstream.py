@@ -50,7 +50,7 @@ class MT19937Stream:
         self.chains = torch.zeros(self.n_chains, MT_N, dtype=torch.int32, device=dev)
         self.prefix = torch.zeros(self.n_chains, PREFIX, dtype=torch.int32, device=dev)
         self.polys = torch.zeros(nk + 1, POLY_WORDS, dtype=torch.int32, device=dev)
-        self.ctl = torch.zeros(4, dtype=torch.int64, device=dev)
+        self.ctl = torch.zeros(6, dtype=torch.int64, device=dev)
         s = _lib.MT19937()
         s.n_chains, s.rounds, s.ring_draws = self.n_chains, self.rounds, self.ring_draws
         s.ring, s.chains, s.prefix = self.ring.data_ptr(), self.chains.data_ptr(), self.prefix.data_ptr()

@@ -535,6 +535,10 @@ class SafeLifeVecEnv:
         d = {"board": self.board.clone(), "goals": self.goals.clone(),
              "start_board": self.start_board.clone(), "step_index": self._step_index,
              "stream_pos": self.stream_pos.clone()}
+        pos = getattr(self.stream_exchange, "pos", None)
+        if pos is not None:
+            # parity mode over shards: the global stream position lives in the exchange
+            d["exchange_pos"] = pos.clone()
         d.update({k: v.clone() for k, v in self.st_t.items()})
         return d
 
@@ -554,6 +558,9 @@ class SafeLifeVecEnv:
             v.copy_(d[k])
         self._step_index = int(d["step_index"])
         self.stream_pos.copy_(d["stream_pos"])
-        if self.mt is not None:
-            self.mt.seek(int(self.stream_pos.item()))
+        pos = getattr(self.stream_exchange, "pos", None)
+        if pos is not None and "exchange_pos" in d:
+            pos.copy_(d["exchange_pos"])
+        if self.mt is not None:      # the next step reads from the (global) position on
+            self.mt.seek(int((pos if pos is not None else self.stream_pos).item()))
         self._invalidate_caches()

@@ -221,3 +221,108 @@ def test_get_obs_arguments_vs_oracle(torch_dev):
             gl = tuple(env.game.agent_loc)
             want = oracle.make_obs(b, env.game.goals, gl[0], gl[1], ex, (33, 33), channels, True)
             assert np.array_equal(env.get_obs(board=b), want), (channels, k)
+
+
+def test_save_rebases_performance(torch_dev, tmp_path):
+    """save() makes the saved state the game's _init_data (safelife_game.py:225):
+    performance_ratio then scores against it (completed 0) and the side-effect start
+    board is the saved board."""
+    from safelife_amd import SafeLifeGame, speedups
+    path = os.path.join(GOLDEN, "pools", "c3_prune_still_64.npz")
+    d = np.load(path)
+    lvl = {k: d[k][2] for k in ("board", "goals", "agent_loc", "orientation", "spawn_prob",
+                                 "min_performance")}
+    speedups.seed(9)
+    game = SafeLifeGame.loaddata(lvl)
+    for a in ["TOGGLE RIGHT", "MOVE UP", "TOGGLE LEFT", "TOGGLE UP"] * 5:
+        game.execute_action(a)
+        game.advance_board()
+    done0, total0 = game.performance_ratio()
+    game.save(str(tmp_path / "mid"))
+    done1, total1 = game.performance_ratio()
+    assert done1 == 0 and total1 == total0 - done0
+    assert np.array_equal(game._venv.start_board[0].cpu().numpy(), game.board)
+    assert np.array_equal(game._init_data["board"], game.board)
+
+
+def test_batch_view_advance_leaves_other_envs(torch_dev):
+    """advance_board on a view of a Philox batch keys its draws on the game's own
+    counter: the batch's step index, and so every other env's later steps, are those
+    of a twin batch whose env was never advanced by hand."""
+    import torch
+    from safelife_amd import SafeLifeGame, SafeLifeVecEnv, LevelPool
+    path = os.path.join(GOLDEN, "pools", "c5_navigation_128.npz")
+    pool = LevelPool.load(path)
+    kw = dict(rng="philox", seed=3, output_channels=None, time_limit=50)
+    v, twin = SafeLifeVecEnv(pool, 6, "cuda:0", **kw), SafeLifeVecEnv(pool, 6, "cuda:0", **kw)
+    v.reset()
+    twin.reset()
+    gv = SafeLifeGame(v, 2)
+    for _ in range(3):
+        gv.advance_board()
+    assert v._step_index == twin._step_index == 0
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(1)
+    for t in range(12):
+        a = torch.randint(0, 9, (6,), dtype=torch.int32, device="cuda:0", generator=g)
+        v.step(a)
+        twin.step(a)
+        keep = [i for i in range(6) if i != 2]
+        assert torch.equal(v.board[keep], twin.board[keep]), t
+        assert torch.equal(v.goals[keep], twin.goals[keep]), t
+
+
+def test_board_setter_on_128_replay_matches_generic(torch_dev):
+    """Assigning game.board on a 128x128 replay env drops the draw planes the last
+    step left (planes_ok bit 3), so the next replay steps count the new board's
+    eligible cells: the bit-sliced replay equals the per-cell kernel's, draw for draw,
+    after the assignment."""
+    import torch
+    from safelife_amd import SafeLifeGame, SafeLifeVecEnv, LevelPool
+    path = os.path.join(GOLDEN, "pools", "c5_navigation_128.npz")
+    pool = LevelPool.load(path)
+    stream = np.random.RandomState(12).random_sample(3_000_000)
+    envs = [SafeLifeVecEnv(pool, 4, "cuda:0", rng="stream", spawn_stream=stream, kernel=k,
+                           output_channels=None, time_limit=200) for k in ("fast", "generic")]
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(2)
+    acts = [torch.randint(0, 9, (4,), dtype=torch.int32, device="cuda:0", generator=g)
+            for _ in range(20)]
+    for e in envs:
+        e.reset()
+        for t in range(5):
+            e.step(acts[t])
+    new = envs[0].board[1].cpu().numpy().copy()
+    new[40:60, 40:60] = 152                  # a block of spawners
+    for e in envs:
+        SafeLifeGame(e, 1).board = new
+    for t in range(5, 20):
+        for e in envs:
+            e.step(acts[t])
+        assert torch.equal(envs[0].board, envs[1].board), t
+        assert torch.equal(envs[0].goals, envs[1].goals), t
+        assert torch.equal(envs[0].stream_pos, envs[1].stream_pos), t
+    assert not envs[0].stream_error()
+
+
+def test_state_dict_keeps_exchange_position(torch_dev):
+    """With a StreamExchange (parity mode over shards) the global stream position is
+    saved and restored with the env."""
+    import torch
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    from safelife_amd import dist as sdist
+    path = os.path.join(GOLDEN, "pools", "c5_navigation_128.npz")
+    pool = LevelPool.load(path)
+    ex = sdist.StreamExchange(device="cuda:0")
+    v = SafeLifeVecEnv(pool, 4, "cuda:0", rng="stream",
+                       spawn_stream=np.random.RandomState(1).random_sample(2_000_000),
+                       stream_exchange=ex, output_channels=None)
+    v.reset()
+    for _ in range(4):
+        v.step(torch.zeros(4, dtype=torch.int32, device="cuda:0"))
+    sd = v.state_dict()
+    p = int(ex.pos.item())
+    assert p > 0 and int(sd["exchange_pos"].item()) == p
+    ex.pos.zero_()
+    v.load_state_dict(sd)
+    assert int(ex.pos.item()) == p

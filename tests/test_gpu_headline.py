@@ -132,23 +132,29 @@ def test_c4_mixed_pool_vs_oracle(torch_dev):
 
 # ------------------------------------------------------ (c) the benchmark regime
 @pytest.mark.parametrize("pool_paths,obs", [((C3,), "none"), ((C3,), "packed"),
+                                            ((C3,), "channels"), ((C3,), "bfloat16"),
                                             ((C4, C3), "none")])
 def test_bench_regime_sampled_vs_oracle(torch_dev, pool_paths, obs):
     """bench.py's regime at full size: 65 536 envs (32 768 for the C4 mix), random
     level order with toroidal rolls, episode clocks staggered over [0, 1000) and a
     400-step burn-in of random actions (boards full of toggled life, resets spread
     over every step), time_limit 1000.  Sampled envs' state is then handed to the
-    oracle, and both run 60 more steps (crossing resets) bit-exact."""
+    oracle, and both run 60 more steps (crossing resets) bit-exact.  obs "channels":
+    the reference's default 15-channel u16 views (safelife_env.py:79, what its PPO
+    consumes), fused into the step kernel; "bfloat16": the same bits as 0.0 / 1.0."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
     levels = _levels(*pool_paths)
     B = 65536 if len(pool_paths) == 1 else 32768
     seed = 1234
-    kw = dict(time_limit=1000, view_shape=(33, 33), output_channels=None, penalty_coef=1.0,
+    chans = obs in ("channels", "bfloat16")
+    kw = dict(time_limit=1000, view_shape=(33, 33),
+              output_channels=tuple(range(15)) if chans else None, penalty_coef=1.0,
               min_performance=0.01)
     venv = SafeLifeVecEnv(LevelPool.load(*pool_paths), B, dev, rng="philox", seed=seed,
                           level_order="random", augment_roll=True, kernel="fast",
-                          compute_obs=obs != "none", **kw)
+                          compute_obs=obs != "none",
+                          obs_dtype="bfloat16" if obs == "bfloat16" else "uint16", **kw)
     venv.reset()
     g = torch.Generator(device=dev)
     g.manual_seed(99)
@@ -183,7 +189,9 @@ def test_bench_regime_sampled_vs_oracle(torch_dev, pool_paths, obs):
             assert bool(vd[e]) == dn, ctx
             assert np.array_equal(venv.board[e].cpu().numpy(), oenvs[e].board), ctx
             assert np.array_equal(venv.goals[e].cpu().numpy(), oenvs[e].goals), ctx
-            if obs != "none":
+            if obs == "bfloat16":
+                assert np.array_equal(vo[e].float().cpu().numpy(), o.astype(np.float32)), ctx
+            elif obs != "none":
                 assert np.array_equal(vo[e].cpu().numpy(), o), ctx
     assert n_reset >= 6
 

@@ -93,7 +93,7 @@ def test_g2_reproduced_from_seed_alone(torch_dev):
         pos = 0
         for t in range(d[key + "_boards"].shape[0]):
             nb, ng = (int(c) for c in speedups.count_eligible(bg).cpu().numpy())
-            draws = mt.draws(pos, nb + ng)
+            draws = mt.draws(pos, max(nb + ng, 1))
             offs = torch.tensor([0, nb], dtype=torch.int64, device=dev)
             bg = speedups.advance_boards(bg, 0.3, rng="stream", draws=draws, draw_offsets=offs)
             pos += nb + ng

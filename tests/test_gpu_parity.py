@@ -359,6 +359,47 @@ def test_fast_kernel_fused_obs(torch_dev, view, remove_white, auto_reset, hi_bit
     assert resets > 0 or not auto_reset
 
 
+@pytest.mark.parametrize("view,channels,dtype,auto_reset,hi_bits", [
+    ((33, 33), tuple(range(15)), "uint16", True, False),
+    ((33, 33), tuple(range(15)), "bfloat16", True, False),
+    ((15, 15), tuple(range(15)), "uint8", True, False),
+    ((33, 33), tuple(range(15)), "float32", True, True),
+    ((33, 33), (0, 3, 5, 9, 10, 11), "uint16", False, False),
+    ((7, 64), (1, 4, 2, 12, 13, 14, 15, 0), "bfloat16", True, False),
+    ((1, 1), tuple(range(16)), "uint8", True, False),
+    ((40, 40), tuple(range(15)), "uint16", True, False)])      # > kFusedChanCells: unfused
+def test_fast_kernel_fused_channel_obs(torch_dev, view, channels, dtype, auto_reset, hi_bits):
+    """Channel views (the reference's default output_channels=range(15), other channel
+    lists, u16 / u8 / f32 / bf16 elements) written by the 64x64 step kernel from the
+    board it holds on chip, and by the reset-list kernel for envs reset after the step,
+    equal every step what the stand-alone observation kernel computes from the state
+    left behind; boards using cell bits 12-14 take the kernel's from-HBM fallback."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv
+    path = os.path.join(GOLDEN, "pools", "c3_prune_still_64.npz")
+    pool = _sprinkled_pool(path, np.random.RandomState(4), spawn_frac=0.006)
+    pool.goals[:, 5:9, 5:9] = 0x0E00 | 0x10
+    if hi_bits:
+        walls = (pool.board & 0x10) != 0
+        pool.board[walls] |= np.uint16(0x7000)
+    B, T = 130, 40
+    venv = SafeLifeVecEnv(pool, B, "cuda:0", kernel="fast", view_shape=view,
+                          output_channels=channels, obs_dtype=dtype, time_limit=17,
+                          auto_reset=auto_reset, rng="philox", seed=31, level_order="random",
+                          augment_roll=True, min_performance=0.01)
+    venv.reset()
+    rng = np.random.RandomState(8)
+    resets = 0
+    for t in range(T):
+        a = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+        o, _, _, info = venv.step(a)
+        fused = o.clone()
+        resets += int(info["reset"].sum().item()) if auto_reset else 0
+        ref = venv.observe().clone()
+        assert torch.equal(fused.view(torch.uint8), ref.view(torch.uint8)), t
+    assert resets > 0 or not auto_reset
+
+
 def test_fast_kernel_spawners_vs_oracle(torch_dev):
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv

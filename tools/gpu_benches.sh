@@ -11,5 +11,5 @@ for spec in "$@"; do
   name=${spec%%:*}; args=${spec#*:}
   timeout -k 10 600 python3 bench.py $args > gpurun_out/$TAG/bench_$name.json 2> gpurun_out/$TAG/bench_$name.err \
       || { echo "$name failed"; tail -5 gpurun_out/$TAG/bench_$name.err; exit 1; }
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], round(d['value']/1e6,2), 'M env-steps/s', r['kernel'], r['kernel_ms'], 'ms frac', r['frac'], 'traffic', r['traffic'])" gpurun_out/$TAG/bench_$name.json $name
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], round(d['value']/1e6,4), 'M env-steps/s', d['ms_per_step'], 'ms/step', r.get('kernel'), r.get('kernel_ms'), 'ms frac', r['frac'], 'traffic', r['traffic'])" gpurun_out/$TAG/bench_$name.json $name
 done
