@@ -350,6 +350,41 @@ __device__ __forceinline__ int lds_cell_idx(int row, int col) {
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
+// Per-half OR: bit y of the result is set when any lane of this lane's parity (rows
+// 32 (lane & 1) + y) has it -- quad xor 2, then two row rotations keep the parity
+__device__ __forceinline__ uint64_t changed_rows64(u32 cl) {
+    u32 x = cl | dpp<0x4E>(cl);           // quad_perm [2,3,0,1]
+    x |= dpp<0x124>(x);                   // row_ror:4
+    x |= dpp<0x128>(x);                   // row_ror:8
+    const u32 lo = (u32)__builtin_amdgcn_readlane((int)x, 0) | (u32)__builtin_amdgcn_readlane((int)x, 16) |
+                   (u32)__builtin_amdgcn_readlane((int)x, 32) | (u32)__builtin_amdgcn_readlane((int)x, 48);
+    const u32 hi = (u32)__builtin_amdgcn_readlane((int)x, 1) | (u32)__builtin_amdgcn_readlane((int)x, 17) |
+                   (u32)__builtin_amdgcn_readlane((int)x, 33) | (u32)__builtin_amdgcn_readlane((int)x, 49);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// The rows of M (bit r = row r) stored from the LDS board (lds_put_board's layout:
+// chunk c of row r at chunk (c + 4 (r >> 5)) & 7), ANDed with `keep`: slot s = lane >> 3
+// of each store instruction takes the s-th listed row, lane & 7 its 16-byte chunk.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_rows(lds_u32 *buf, uint8_t *rowlist, u32 *gb0, uint64_t M,
+                                           u32 keep, int lane) {
+    typedef __attribute__((address_space(3))) uint8_t lds_u8;
+    typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+    lds_u8 *rl = (lds_u8 *)rowlist;
+    if ((M >> lane) & 1ull) rl[lanes_below(M)] = (uint8_t)lane;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int n = __builtin_popcountll(M);
+    const int c = lane & 7;
+    for (int s = lane >> 3; s < n; s += 8) {
+        const int row = rl[s];
+        u32x4 v = *(const lds_u32x4 *)(buf + row * 32 + (((c + 4 * (row >> 5)) & 7) << 2));
+        v &= keep;
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(gb0) + row * 8 + c);
+    }
+}
+
 // exit y (R_EY) or x (R_EX) number e of the record, e = this lane's own index
 __device__ __forceinline__ int lane_exit(const RecFields &fl, int e, int field) {
     const u32 w = (u32)__builtin_amdgcn_ds_bpermute(4 * (field + (e >> 1)), (int)fl.V);
@@ -494,7 +529,8 @@ __device__ __forceinline__ void issue_pre(const sl_env_state &st, const int32_t 
 template <int OBS, int MODE>
 __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs &a,
                                          const FastExtra &fx, int64_t b, int lane, lds_u32 *buf,
-                                         uint16_t *vm, const int32_t *__restrict__ actions,
+                                         uint16_t *vm, uint8_t *rowlist,
+                                         const int32_t *__restrict__ actions,
                                          int ctp, int ctc, double *reward_out, uint8_t *done_out,
                                          uint8_t *flags_out, int32_t *ep_len_out,
                                          int32_t *ep_rew_out, const Pre &pre) {
@@ -671,13 +707,21 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
             PL(PB, 9, w) = can ? (PL(PB, 9, w) | PL(PB, 8, w)) : (PL(PB, 9, w) & ~PL(PB, 8, w));
         transpose32(PB);
         if (VIEW && !hi) {
-            // planes 12-14 hold the goal colours: the store masks them out again
-            if (rb) {
-#pragma unroll
-                for (int y = 0; y < 32; y++)
-                    if ((rb >> y) & 1u) gb[y * 32] = PB[y] & 0x8FFF8FFFu;
-            }
             lds_put_board(buf, lane, PB);      // the start board in buf has been read out
+            // the changed rows from the LDS board (which the views read anyway), 8 whole
+            // rows per store; planes 12-14 hold the goal colours: the store masks them
+            // out again.  (From registers a store writes rows y and 32 + y together:
+            // same box, packed views 264.5 vs 258.9 M env-steps/s, tools/ab/c3_rowlist.py;
+            // without views the LDS round trip costs more than the bytes it saves,
+            // 344.6 vs 356.7 M, so that path keeps the register stores below.)
+            if (rb) {
+                uint64_t M = changed_rows64(cb[0] | cb[1]);
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (k < ne) M |= 1ull << (eidx[k] >> 6);
+                store_rows(buf, rowlist, reinterpret_cast<u32 *>(st.board + off), M, 0x8FFF8FFFu,
+                           lane);
+            }
         } else if (rb) {
 #pragma unroll
             for (int y = 0; y < 32; y++)
@@ -734,11 +778,12 @@ k_env_step_bits64(StepKArgs ka) {
     __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
     // channel views: the view's channel masks (write_obs_channels)
     __shared__ __attribute__((aligned(16))) uint16_t vmask[OBS >= 2 ? sl::obs::kFusedChanCells : 2];
+    __shared__ uint8_t rowlist[OBS ? 64 : 1];   // changed rows by rank (store_rows)
     lds_u32 *buf = (lds_u32 *)&stage[0];
     Pre pre;
     issue_pre(ka.st, ka.actions, b, lane, pre);
     dma_board(ka.st.board + b * (int64_t)(N * N), buf, lane);
-    step_env<OBS, MODE>(ka.st, ka.a, ka.fx, b, lane, buf, vmask, ka.actions, ka.ctp, ka.ctc,
+    step_env<OBS, MODE>(ka.st, ka.a, ka.fx, b, lane, buf, vmask, rowlist, ka.actions, ka.ctp, ka.ctc,
                         ka.reward_out, ka.done_out, ka.flags_out, ka.ep_len_out, ka.ep_rew_out,
                         pre);
 }

@@ -39,8 +39,8 @@ def test_labels():
     assert bench.metric_name(64, 64, 65536) == json.load(
         open(os.path.join(REPO, "BASELINE.json")))["metric"]
     assert "25×25" in bench.metric_name(25, 25, 4096)
-    assert bench.step_kernel_name(64, 64, "none", "auto") == "k_env_step_bits64<false, 0>"
-    assert bench.step_kernel_name(64, 64, "packed", "auto") == "k_env_step_bits64<true, 0>"
+    assert bench.step_kernel_name(64, 64, "none", "auto") == "k_env_step_bits64<0, 0>"
+    assert bench.step_kernel_name(64, 64, "packed", "auto") == "k_env_step_bits64<1, 0>"
     assert bench.step_kernel_name(25, 25, "none", "auto") == "k_env_step_seg4<0, true>"
     assert bench.step_kernel_name(25, 29, "none", "auto") == "k_env_step_seg4<0, false>"
     assert bench.step_kernel_name(25, 40, "none", "auto") == "k_env_step_small<0>"
@@ -48,25 +48,31 @@ def test_labels():
     assert (bench.step_kernel_name(128, 128, "none", "auto", "stream")
             == "k_env_step_bits128<3>")                  # draws decided before the step
     assert (bench.step_kernel_name(64, 64, "none", "auto", "stream")
-            == "k_env_step_bits64<false, 1>")
+            == "k_env_step_bits64<0, 1>")
     # replay without any spawner runs the Philox form
     assert (bench.step_kernel_name(64, 64, "none", "auto", "stream", replay=False)
-            == "k_env_step_bits64<false, 0>")
+            == "k_env_step_bits64<0, 0>")
     assert bench.step_kernel_name(64, 64, "none", "generic") == "k_env_step_generic"
+    # channel views are written by the step kernel (obs_kind 2: u16 / bf16, 3: u8, 4: f32)
+    assert bench.step_kernel_name(64, 64, "channels", "auto") == "k_env_step_bits64<2, 0>"
+    assert (bench.step_kernel_name(64, 64, "channels", "auto", obs_dtype="bfloat16")
+            == "k_env_step_bits64<2, 0>")
+    assert (bench.step_kernel_name(64, 64, "channels", "auto", obs_dtype="uint8")
+            == "k_env_step_bits64<3, 0>")
 
 
 def test_pmc_record_keyed_on_build(tmp_path, monkeypatch):
     prof = tmp_path / "profiles"
     prof.mkdir()
-    rec = {"kernel": "void k_env_step_bits64<false, 0>(StepKArgs)", "build_id": "abc",
+    rec = {"kernel": "void k_env_step_bits64<0, 0>(StepKArgs)", "build_id": "abc",
            "hbm_bytes_per_launch": 123.0, "profile": "rX"}
     (prof / "pmc_c3.json").write_text(json.dumps(rec))
     monkeypatch.setattr(bench, "REPO", str(tmp_path))
-    assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits64<false, 0>")[0] == 123.0
+    assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits64<0, 0>")[0] == 123.0
     # replay lines keep their own record
-    assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits64<false, 0>",
+    assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits64<0, 0>",
                                      "stream")[0] is None
-    assert bench.traffic_from_record("c3", "none", "other", "k_env_step_bits64<false, 0>")[0] is None
+    assert bench.traffic_from_record("c3", "none", "other", "k_env_step_bits64<0, 0>")[0] is None
     assert bench.traffic_from_record("c3", "none", "abc", "k_env_step_bits128<0>")[0] is None
     assert bench.traffic_from_record("c5", "none", "abc", "k_env_step_bits128<0>")[0] is None
 

@@ -39,6 +39,20 @@ def derive(d):
     if "SQ_INSTS_VALU" in d and d.get("SQ_WAVES"):
         d["valu_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
         d["salu_per_wave"] = d.get("SQ_INSTS_SALU", 0) / d["SQ_WAVES"]
+    # wave-cycle attribution (MI355X_MICROARCH.md, PMC slots): WAVE_CYCLES = WAIT_ANY
+    # (parked on s_waitcnt / barrier) + WAIT_INST_ANY (issue-stalled) + ACTIVE_INST_ANY
+    # (issuing), all in quad-cycles; ACTIVE_INST_<unit> split the issuing part
+    wc = d.get("SQ_WAVE_CYCLES")
+    if wc:
+        att = {}
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS",
+                  "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS",
+                  "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_FLAT", "SQ_ACTIVE_INST_MISC"):
+            if k in d:
+                att[k[3:].lower() + "_frac"] = round(d[k] / wc, 4)
+        if d.get("SQ_WAVES"):
+            att["wave_life_cycles"] = round(4 * wc / d["SQ_WAVES"], 1)
+        d["wave_cycle_attribution"] = att
 
 
 def main(out, last=0):
