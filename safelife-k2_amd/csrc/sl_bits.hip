@@ -303,6 +303,184 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
     }
 }
 
+// ---------------------------------------------------------------- tail resets
+// The resets of the envs a step finished, inside the step's own launch (round 4): the
+// grid carries fx.tail_workers workgroups after the B step waves.  A step wave whose
+// env finished publishes it -- its stores, then an agent-scope release (its XCD's L2
+// written back, so that the reset's stores, from whichever XCD, land after the
+// step's), then a list slot and a 64-bit entry tagged with the step -- and every step
+// wave counts itself done.  The workers take entries as they appear and leave once
+// all B step waves are done and the list is drained, so the resets run in the step's
+// tail instead of after it.  Placement-independent (MI355X_MICROARCH.md,
+// inter-workgroup visibility): no dispatch order or co-location is assumed (workers
+// dispatched early only spin longer), and every spin is bounded (error bit 2).
+// The reset reads nothing the step wrote (episodes, the pool, the arguments), so the
+// workers' acquire only guards their own CU's L1.
+constexpr int kDoneShards = 4;
+constexpr int kTailWorkers = 64;
+constexpr int kTailSpins = 1 << 18;    // ~0.5 s of polling before a worker gives up
+struct TailWords {
+    int64_t *cnt, *done, *next_cnt, *next_done, *err;
+    uint64_t *list;
+};
+__device__ __forceinline__ TailWords tail_words(int64_t *scratch, int64_t B, uint32_t step) {
+    int64_t *base = scratch + 8 * B;
+    const int p = (int)(step & 1u);
+    return TailWords{base + 2 + p, base + 4 + kDoneShards * p, base + 2 + (p ^ 1),
+                     base + 4 + kDoneShards * (p ^ 1), base,
+                     reinterpret_cast<uint64_t *>(scratch)};
+}
+__device__ __forceinline__ uint32_t tail_tag(uint32_t step) { return step + 1u; }
+
+template <class T>
+__device__ __forceinline__ T ld_agent(T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the step wave's side (all lanes; reset wave-uniform)
+__device__ __forceinline__ void tail_publish(int64_t *scratch, int64_t B, uint32_t step, int64_t b,
+                                             int reset, int lane) {
+    const TailWords tw = tail_words(scratch, B, step);
+    if (reset) {
+        wait_vm();                  // every lane's stores of this step have completed
+        if (lane == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            wait_vm();
+            const int64_t slot = __hip_atomic_fetch_add(tw.cnt, (int64_t)1, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&tw.list[slot], ((uint64_t)tail_tag(step) << 32) | (uint64_t)b,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        wait_vm();                  // the entry is out before this wave counts as done
+    }
+    if (lane == 0)
+        __hip_atomic_fetch_add(&tw.done[b % kDoneShards], (int64_t)1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A pool level into the wave's LDS board buffer with its rows rolled by dy: LDS row r
+// (128 bytes, columns unrolled, no chunk rotation) is level row (r - dy) & 63.  Each
+// DMA instruction fills 8 LDS rows; the roll is in the per-lane source addresses.
+__device__ __forceinline__ void dma_level_rolled(const uint16_t *__restrict__ src, lds_u32 *buf,
+                                                 int lane, int dy) {
+    const char *s = reinterpret_cast<const char *>(src);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int r = 8 * k + (lane >> 3);
+        __builtin_amdgcn_global_load_lds((const void *)(s + ((r - dy) & 63) * 128 + (lane & 7) * 16),
+                                         (__attribute__((address_space(3))) void *)(buf + k * 256),
+                                         16, 0, 0);
+    }
+}
+
+// wave_reset within the step kernel's register budget (tail_worker): the same result.
+// The level's goals, then its board, are DMA'd row-rolled into the wave's LDS board
+// buffer (dma_level_rolled) and each lane reads its rolled column pair from there at
+// two base addresses plus immediate row offsets, so that no gather addresses are held
+// and a board's rows and its planes are never live together.
+__device__ __forceinline__ void wave_reset_lean(const sl_env_state &st, const sl_level_pool &pool,
+                                                const ResetArgs &ra, int64_t b, int lane,
+                                                lds_u32 *buf) {
+    const int ep = __builtin_amdgcn_readfirstlane(st.episodes[b]);
+    const LevelChoice lc = choose_level_wave(pool, ra, ra.env0 + (uint32_t)b, ep, N, N, lane);
+    const int li = __builtin_amdgcn_readfirstlane(lc.idx);
+    const int dy = __builtin_amdgcn_readfirstlane(lc.dy), dx = __builtin_amdgcn_readfirstlane(lc.dx);
+    const LevelScalars ls = level_scalars(pool, li);
+    const int h = lane & 1, j = lane >> 1;
+    const uint16_t *lb = pool.board + (int64_t)li * (N * N), *lg = pool.goals + (int64_t)li * (N * N);
+    const int c0 = (2 * j - dx) & 63, c1 = (2 * j + 1 - dx) & 63;
+    const int64_t off = b * (int64_t)(N * N);
+    const uint32_t lane_off = (uint32_t)(h * 1024 + j);
+    u32 *gs = reinterpret_cast<u32 *>(st.start_board + off);
+    u32 *gg = reinterpret_cast<u32 *>(st.goals + off);
+    u32 *gb = reinterpret_cast<u32 *>(st.board + off);
+    typedef __attribute__((address_space(3))) const uint16_t lds_cu16_t;
+    lds_cu16_t *q0 = reinterpret_cast<lds_cu16_t *>(buf) + 32 * h * N + c0;
+    lds_cu16_t *q1 = reinterpret_cast<lds_cu16_t *>(buf) + 32 * h * N + c1;
+    auto rolled = [&](u32 D[32]) {
+#pragma unroll
+        for (int y = 0; y < 32; y++) D[y] = (u32)q0[y * N] | ((u32)q1[y * N] << 16);
+    };
+    dma_level_rolled(lg, buf, lane, dy);
+    wait_vm();
+    u32 P[32];
+    rolled(P);
+    wait_lgkm();                    // the goals are read out of the buffer
+    dma_level_rolled(lb, buf, lane, dy);    // under the goals' stores and sums
+#pragma unroll
+    for (int y = 0; y < 32; y++) gg[lane_off + y * 32] = P[y];
+    transpose32(P);
+    if (st.planes) {
+        u32 *mg = st.planes + b * 4096 + 2048;
+#pragma unroll
+        for (int q = 0; q < 32; q++) mg[(uint32_t)(q * 64 + lane)] = P[q];
+    }
+    u32 gcol[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        gcol[k][0] = PL(P, 9 + k, 0);
+        gcol[k][1] = PL(P, 9 + k, 1);
+    }
+    const bool sg = __ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull;
+    wait_vm();
+    rolled(P);
+#pragma unroll
+    for (int y = 0; y < 32; y++) gs[lane_off + y * 32] = P[y];
+    transpose32(P);
+    int pts, scr, pos, side;
+    score_planes(P, gcol, P, &pts, &scr, &pos, &side);
+    const int s1 = wave_total((pts + 192) | ((scr + 64) << 16));
+    const int s2 = wave_total(pos);
+    const bool sb = __ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull;
+    const u32 ex0 = PL(P, 8, 0), ex1 = PL(P, 8, 1);
+    int ev = 0;
+    if (lane == 0)
+        ev = reset_scalars_from(st, ra, b, li, dy, dx, ls, ep, (s1 & 0xFFFF) - 192 * 64,
+                                ((s1 >> 16) & 0xFFFF) - 64 * 64, s2, (sb ? 1 : 0) | (sg ? 2 : 0));
+    ev = __builtin_amdgcn_readfirstlane(ev);
+    asm volatile("" ::: "memory");  // read the rows again (not kept through the sums)
+    rolled(P);
+#pragma unroll
+    for (int y = 0; y < 32; y++) {
+        u32 d = P[y];
+        if (d & (u32)EXIT) d = (d & 0xFFFF0000u) | (u32)ev;
+        if (d & ((u32)EXIT << 16)) d = (d & 0x0000FFFFu) | ((u32)ev << 16);
+        gb[lane_off + y * 32] = d;
+    }
+    const int n_exit = wave_total(__builtin_popcount(ex0) + __builtin_popcount(ex1));
+    {
+        u32 e0 = ex0, e1 = ex1;
+        const int kmax = n_exit < SL_MAX_EXITS ? n_exit : SL_MAX_EXITS;
+        for (int k = 0; k < kmax; k++) {
+            const u32 k0 = e0 ? (u32)((32 * h + __builtin_ctz(e0)) * N + 2 * j) : 0xFFFFu;
+            const u32 k1 = e1 ? (u32)((32 * h + __builtin_ctz(e1)) * N + 2 * j + 1) : 0xFFFFu;
+            u32 m = k0 < k1 ? k0 : k1;
+            m = min(m, dpp<0xB1>(m));
+            m = min(m, dpp<0x4E>(m));
+            m = min(m, dpp<0x141>(m));
+            m = min(m, dpp<0x140>(m));
+            const u32 key = min(min((u32)__builtin_amdgcn_readlane((int)m, 0),
+                                    (u32)__builtin_amdgcn_readlane((int)m, 16)),
+                                min((u32)__builtin_amdgcn_readlane((int)m, 32),
+                                    (u32)__builtin_amdgcn_readlane((int)m, 48)));
+            if (k0 == key) e0 &= e0 - 1;
+            if (k1 == key) e1 &= e1 - 1;
+            if (lane == 0) {
+                st.exit_y[b * SL_MAX_EXITS + k] = (int16_t)(key >> 6);
+                st.exit_x[b * SL_MAX_EXITS + k] = (int16_t)(key & 63);
+            }
+        }
+    }
+    if (lane == 0) {
+        if (st.planes) st.planes_ok[b] = 2;
+        st.exit_count[b] = n_exit;
+        for (int e = n_exit; e < SL_MAX_EXITS; e++) {
+            st.exit_y[b * SL_MAX_EXITS + e] = 0;
+            st.exit_x[b * SL_MAX_EXITS + e] = 0;
+        }
+    }
+}
+
 // all kernel arguments of k_env_step_bits64 in one struct at kernarg offset 0, so a
 // phase can re-read one late through kernarg() (write_obs)
 struct StepKArgs {
@@ -324,6 +502,7 @@ __device__ __forceinline__ const StepKArgs &kernarg() {
     asm volatile("" : "+s"(kp));
     return *(const StepKArgs *)kp;
 }
+__device__ __forceinline__ const sl_env_state &st_of_kernarg() { return kernarg().st; }
 
 // ---------------------------------------------------------------- fused observation
 // SafeLifeEnv.get_obs + recenter_view (safelife_env.py:125-155, helper_utils.py:41-74)
@@ -760,7 +939,9 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         else
             sl::obs::obs_packed_wave(st, oa, b, lane, lfx.obs_out);
     }
-    if (fx.fuse_reset && reset && lane == 0) {
+    if (fx.tail_workers) {
+        tail_publish(fx.scratch, st.B, a.step, b, reset, lane);
+    } else if (fx.fuse_reset && reset && lane == 0) {
         // queue the env for the reset kernel (k_env_reset_list)
         int64_t *cnt = fx.scratch + 8 * st.B + 2 + (a.step & 1);
         const int i = (int)atomicAdd((unsigned long long *)cnt, 1ull);
@@ -768,10 +949,89 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     }
 }
 
+// the view of a reset env, from its stored state (this wave's own stores, landed)
+__device__ __forceinline__ void reset_view(const FastExtra &fx, int64_t b, int lane, uint16_t *vm) {
+    wait_vm();
+    sl::obs::ObsArgs oa{};
+    oa.vh = fx.obs_vh;
+    oa.vw = fx.obs_vw;
+    oa.remove_white = fx.obs_rw;
+    oa.mode = fx.obs_mode;
+    oa.nch = fx.obs_nch;
+    const sl::obs::ChanMap cm{fx.obs_chpack, oa.nch};
+    uint8_t *o8 = reinterpret_cast<uint8_t *>(fx.obs_out);
+    if (oa.mode == SL_OBS_PACKED)
+        sl::obs::obs_packed_wave(st_of_kernarg(), oa, b, lane, fx.obs_out);
+    else if (oa.mode == SL_OBS_CHANNELS_U8)
+        sl::obs::obs_channels_wave<1>(st_of_kernarg(), oa, cm, fx.obs_one, b, lane, vm, o8);
+    else if (oa.mode == SL_OBS_CHANNELS_F32)
+        sl::obs::obs_channels_wave<4>(st_of_kernarg(), oa, cm, fx.obs_one, b, lane, vm, o8);
+    else
+        sl::obs::obs_channels_wave<2>(st_of_kernarg(), oa, cm, fx.obs_one, b, lane, vm, o8);
+}
+
+template <int OBS>
+__device__ __forceinline__ void tail_reset_one(int64_t b, int lane, lds_u32 *buf, uint16_t *vm) {
+    const StepKArgs &kb = kernarg();
+    wave_reset_lean(kb.st, kb.fx.pool, kb.fx.ra, b, lane, buf);
+    if (OBS) reset_view(kernarg().fx, b, lane, vm);
+}
+
+// A tail worker (workgroup B + w of the step launch): entries w, w + n, w + 2n, ...
+// of this step's list, each reset as k_env_reset_list does.
+template <int OBS>
+__device__ __forceinline__ void tail_worker(int w, int lane, lds_u32 *buf, uint16_t *vm) {
+    const StepKArgs &ka = kernarg();
+    const int64_t B = ka.st.B;
+    const uint32_t step = ka.a.step;
+    const TailWords tw = tail_words(ka.fx.scratch, B, step);
+    const int n = (int)gridDim.x - (int)B;
+    if (w == 0 && lane == 0) {      // the next step's counters
+        *tw.next_cnt = 0;
+#pragma unroll
+        for (int k = 0; k < kDoneShards; k++) tw.next_done[k] = 0;
+    }
+    int spins = kTailSpins;
+    for (int k = w;; k += n) {
+        bool have = false;
+        for (;;) {
+            if (__builtin_amdgcn_readfirstlane((int)ld_agent(tw.cnt)) > k) {
+                have = true;
+                break;
+            }
+            int64_t d = 0;
+#pragma unroll
+            for (int s = 0; s < kDoneShards; s++) d += ld_agent(&tw.done[s]);
+            if (__builtin_amdgcn_readfirstlane((int)d) >= B) {
+                have = __builtin_amdgcn_readfirstlane((int)ld_agent(tw.cnt)) > k;
+                break;
+            }
+            if (--spins < 0) break;
+            __builtin_amdgcn_s_sleep(16);
+        }
+        uint64_t e = 0;
+        while (have) {
+            e = ld_agent(&tw.list[k]);
+            if ((uint32_t)__builtin_amdgcn_readfirstlane((int)(e >> 32)) == tail_tag(step)) break;
+            if (--spins < 0) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (spins < 0) {
+            if (lane == 0) atomicOr((unsigned long long *)tw.err, 4ull);
+            return;
+        }
+        if (!have) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        wait_vm();
+        const int64_t b = __builtin_amdgcn_readfirstlane((int)(uint32_t)e);
+        tail_reset_one<OBS>(b, lane, buf, vm);
+    }
+}
+
 // OBS: also write the observation (fx.obs_out): 1 packed, 2-4 channel views
 // (obs_esz); MODE: see step_env
 template <int OBS, int MODE>
-__global__ void __launch_bounds__(64, (OBS || MODE == SPAWN_STREAM) ? kMinWavesObs : kMinWaves)
+__global__ void __launch_bounds__(64, MODE == SPAWN_STREAM ? kMinWavesObs : kMinWaves)
 k_env_step_bits64(StepKArgs ka) {
     const int64_t b = blockIdx.x;          // one wave per env
     const int lane = threadIdx.x;
@@ -780,6 +1040,10 @@ k_env_step_bits64(StepKArgs ka) {
     __shared__ __attribute__((aligned(16))) uint16_t vmask[OBS >= 2 ? sl::obs::kFusedChanCells : 2];
     __shared__ uint8_t rowlist[OBS ? 64 : 1];   // changed rows by rank (store_rows)
     lds_u32 *buf = (lds_u32 *)&stage[0];
+    if (b >= ka.st.B) {                    // a tail worker
+        tail_worker<OBS>((int)(b - ka.st.B), lane, buf, vmask);
+        return;
+    }
     Pre pre;
     issue_pre(ka.st, ka.actions, b, lane, pre);
     dma_board(ka.st.board + b * (int64_t)(N * N), buf, lane);
@@ -851,7 +1115,12 @@ k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scr
     // channel views of the reset envs: their masks
     __shared__ __attribute__((aligned(16))) uint16_t vmask[sl::obs::kFusedChanCells];
     int64_t *cnt = scratch + 8 * st.B + 2;
-    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(step + 1) & 1] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        cnt[(step + 1) & 1] = 0;
+        // and the tail resets' done counters of that parity (a step with a capture runs
+        // this kernel between steps that use tail_worker)
+        for (int k = 0; k < kDoneShards; k++) cnt[2 + kDoneShards * ((step + 1) & 1) + k] = 0;
+    }
     const int32_t *list = reset_list(scratch);
     // the first entry is loaded together with the length (grid <= B <= list size; the
     // value is used only when the entry is in the list)
@@ -907,8 +1176,12 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (st.H != N || st.W != N) return SL_ETOOBIG;
+    // resets in the step launch's tail (tail_worker), unless a capture needs the frame
+    // between the step and its resets (then the reset-list kernel, as before)
+    StepKArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
+    ka.fx.tail_workers = (fx.fuse_reset && fx.pool.K > 0 && !fx.capture && st.B < (1ll << 31))
+                             ? kTailWorkers : 0;
     const unsigned grid = (unsigned)st.B;
-    const StepKArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
     if (fx.obs_out && (fx.obs_vh < 1 || fx.obs_vw < 1 || fx.obs_vh * fx.obs_vw > 4096))
         return SL_EINVAL;
     if (fx.stream) {
@@ -921,10 +1194,10 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         const int rc = stream_offsets(st, fx, s);
         if (rc || !stream_steps(fx)) return rc;
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        launch_bits64<SPAWN_STREAM>(obs_kind(fx), grid, ka, s);
+        launch_bits64<SPAWN_STREAM>(obs_kind(fx), grid + ka.fx.tail_workers, ka, s);
     } else {
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        launch_bits64<SPAWN_PHILOX>(obs_kind(fx), grid, ka, s);
+        launch_bits64<SPAWN_PHILOX>(obs_kind(fx), grid + ka.fx.tail_workers, ka, s);
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);
@@ -932,7 +1205,7 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         const int rc = launch_capture(st, *fx.capture, flags, 0, s);
         if (rc) return rc;
     }
-    if (fx.fuse_reset && fx.pool.K > 0) {
+    if (fx.fuse_reset && fx.pool.K > 0 && !ka.fx.tail_workers) {
         const unsigned grid = (unsigned)(st.B < 512 ? st.B : 512);
         sl::obs::ObsArgs oa{};
         oa.vh = fx.obs_vh;

@@ -18,6 +18,10 @@ namespace sl {
 //   [8B]      error flags (bit0: draw stream exhausted)
 //   [8B+2], [8B+3]  reset-list lengths for even / odd steps (each step's reset
 //             kernel zeroes the other one)
+//   [8B+4, 8B+12)  64x64 tail resets (sl_bits.hip): per step parity, kDoneShards
+//             counters of the step waves that are done (the tail workers zero the
+//             other parity's); the list is then [0, B) as 64-bit entries tagged with
+//             the step
 struct Scratch {
     int64_t *counts, *offsets, *act, *err;
 };
@@ -332,6 +336,8 @@ struct FastExtra {
     const int64_t *stream_base;   // *stream_base + the step
     const sl_mt19937 *mt;   // replay from the device generator (sl_env_cfg.mt) or NULL:
                             // stream_offsets fills its ring for the step's range
+    int32_t tail_workers = 0;   // 64x64: workgroups after the B step waves that reset the
+                                // envs the step finished, inside the same launch
 };
 // replay-mode phases of a bit-sliced launcher: whether it runs the action + count
 // prologue, and whether it continues past the offsets scan to the step kernel

@@ -427,14 +427,14 @@ class SafeLifeVecEnv:
         self.global_counter.num_steps += self.B
 
     def _check_reset_lists(self):
-        """Zero the per-parity reset-list lengths (scratch[8B+2 : 8B+4]) unless this
-        step directly follows an auto-reset step: each step's reset kernel zeroes
-        only the other parity's list (sl_env_common.h, Scratch)."""
+        """Zero the per-parity reset-list lengths and tail-reset counters
+        (scratch[8B+2 : 8B+12]) unless this step directly follows an auto-reset step:
+        each step zeroes only the other parity's (sl_env_common.h, Scratch)."""
         cur = (self._step_index, self.auto_reset)
         last = self._last_step
         if not (self.auto_reset and last is not None and last[1]
                 and last[0] + 1 == self._step_index):
-            self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()
+            self.scratch[8 * self.B + 2:8 * self.B + 12].zero_()
         self._last_step = cur
 
     def _fill_obs_cfg(self, cfg, out):
@@ -504,6 +504,11 @@ class SafeLifeVecEnv:
         device generator for a range it could not serve)."""
         return bool(self.scratch[8 * self.B].item() & 1)
 
+    def reset_error(self):
+        """True if a 64x64 step's in-launch resets (tail workers, sl_bits.hip) gave up
+        waiting for the step's waves (a bounded spin ran out): envs may be unreset."""
+        return bool(self.scratch[8 * self.B].item() & 4)
+
     def set_state(self, board, goals, start_board, **scalars):
         """Load explicit state (for tests / checkpoints).  Arrays are [B,...]."""
         torch = self.torch
@@ -525,7 +530,7 @@ class SafeLifeVecEnv:
         self.st_t["spawn_flags"].copy_(3 | 4 * hi.to(self.st_t["spawn_flags"].dtype))
         self._may_spawn = True
         self.planes_ok.zero_()
-        self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()
+        self.scratch[8 * self.B + 2:8 * self.B + 12].zero_()
         self._last_step = None
         self._synced = (int(self.st_t["episodes"].sum().item()),
                         int(self.st_t["episodes"].sum().item())

@@ -194,6 +194,56 @@ def test_bench_regime_sampled_vs_oracle(torch_dev, pool_paths, obs):
             elif obs != "none":
                 assert np.array_equal(vo[e].cpu().numpy(), o), ctx
     assert n_reset >= 6
+    assert not venv.reset_error()
+
+
+@pytest.mark.parametrize("obs", ["none", "channels"])
+def test_mass_reset_in_step_tail(torch_dev, obs):
+    """Every env finishes on the same step: 8 192 resets in one launch, far more than
+    its tail workers (sl_bits.hip tail_worker: 64 workgroups, each looping over list
+    entries), with the rest of the batch still stepping beside them.  Sampled envs
+    bit-exact with the oracle over the reset and the steps after it; every env's
+    episode counter advanced exactly once."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    levels = _levels(C3)
+    B, seed, T = 8192, 77, 6
+    kw = dict(time_limit=T, view_shape=(33, 33),
+              output_channels=tuple(range(15)) if obs == "channels" else None,
+              penalty_coef=1.0, min_performance=0.01)
+    venv = SafeLifeVecEnv(LevelPool.load(C3), B, dev, rng="philox", seed=seed,
+                          level_order="random", augment_roll=True, kernel="fast",
+                          compute_obs=obs != "none", **kw)
+    venv.reset()
+    sample = [0, 1, 63, 64, 4095, B - 1]
+    oenvs = {}
+    for e in sample:
+        o = oracle.OracleEnv(oracle.pool_level_fn(levels, e, seed=seed, random_order=True,
+                                                  augment=True),
+                             env_id=e, rng="philox", seed=seed, **kw)
+        o.load_state(_env_state(venv, e), venv._step_index)
+        oenvs[e] = o
+    rng = np.random.RandomState(3)
+    ep0 = venv.st_t["episodes"].clone()
+    most = 0
+    for t in range(T + 3):
+        acts = rng.randint(0, 9, size=B).astype(np.int32)
+        vo, vr, vd, info = venv.step(torch.from_numpy(acts).to(dev))
+        vr, vd = vr.cpu().numpy(), vd.cpu().numpy()
+        for e in sample:
+            o, r, dn, _ = oenvs[e].step(int(acts[e]))
+            ctx = (t, e)
+            assert vr[e] == r, (ctx, vr[e], r)
+            assert bool(vd[e]) == dn, ctx
+            assert np.array_equal(venv.board[e].cpu().numpy(), oenvs[e].board), ctx
+            assert np.array_equal(venv.goals[e].cpu().numpy(), oenvs[e].goals), ctx
+            if obs != "none":
+                assert np.array_equal(vo[e].cpu().numpy(), o), ctx
+        most = max(most, int(vd.sum()))
+    assert most >= B * 9 // 10, most        # (nearly) every env timed out on one step
+    assert not venv.reset_error()
+    n_ep = (venv.st_t["episodes"] - ep0).cpu().numpy()
+    assert n_ep.min() >= 1 and n_ep.max() <= 2
 
 
 # ------------------------------------------------------------- (e) shard layouts
