@@ -303,61 +303,6 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
     }
 }
 
-// ---------------------------------------------------------------- tail resets
-// The resets of the envs a step finished, inside the step's own launch (round 4): the
-// grid carries fx.tail_workers workgroups after the B step waves.  A step wave whose
-// env finished publishes it -- its stores, then an agent-scope release (its XCD's L2
-// written back, so that the reset's stores, from whichever XCD, land after the
-// step's), then a list slot and a 64-bit entry tagged with the step -- and every step
-// wave counts itself done.  The workers take entries as they appear and leave once
-// all B step waves are done and the list is drained, so the resets run in the step's
-// tail instead of after it.  Placement-independent (MI355X_MICROARCH.md,
-// inter-workgroup visibility): no dispatch order or co-location is assumed (workers
-// dispatched early only spin longer), and every spin is bounded (error bit 2).
-// The reset reads nothing the step wrote (episodes, the pool, the arguments), so the
-// workers' acquire only guards their own CU's L1.
-constexpr int kDoneShards = 4;
-constexpr int kTailWorkers = 64;
-constexpr int kTailSpins = 1 << 18;    // ~0.5 s of polling before a worker gives up
-struct TailWords {
-    int64_t *cnt, *done, *next_cnt, *next_done, *err;
-    uint64_t *list;
-};
-__device__ __forceinline__ TailWords tail_words(int64_t *scratch, int64_t B, uint32_t step) {
-    int64_t *base = scratch + 8 * B;
-    const int p = (int)(step & 1u);
-    return TailWords{base + 2 + p, base + 4 + kDoneShards * p, base + 2 + (p ^ 1),
-                     base + 4 + kDoneShards * (p ^ 1), base,
-                     reinterpret_cast<uint64_t *>(scratch)};
-}
-__device__ __forceinline__ uint32_t tail_tag(uint32_t step) { return step + 1u; }
-
-template <class T>
-__device__ __forceinline__ T ld_agent(T *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// the step wave's side (all lanes; reset wave-uniform)
-__device__ __forceinline__ void tail_publish(int64_t *scratch, int64_t B, uint32_t step, int64_t b,
-                                             int reset, int lane) {
-    const TailWords tw = tail_words(scratch, B, step);
-    if (reset) {
-        wait_vm();                  // every lane's stores of this step have completed
-        if (lane == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            wait_vm();
-            const int64_t slot = __hip_atomic_fetch_add(tw.cnt, (int64_t)1, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&tw.list[slot], ((uint64_t)tail_tag(step) << 32) | (uint64_t)b,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        wait_vm();                  // the entry is out before this wave counts as done
-    }
-    if (lane == 0)
-        __hip_atomic_fetch_add(&tw.done[b % kDoneShards], (int64_t)1, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // A pool level into the wave's LDS board buffer with its rows rolled by dy: LDS row r
 // (128 bytes, columns unrolled, no chunk rotation) is level row (r - dy) & 63.  Each
 // DMA instruction fills 8 LDS rows; the roll is in the per-lane source addresses.
@@ -373,11 +318,13 @@ __device__ __forceinline__ void dma_level_rolled(const uint16_t *__restrict__ sr
     }
 }
 
-// wave_reset within the step kernel's register budget (tail_worker): the same result.
-// The level's goals, then its board, are DMA'd row-rolled into the wave's LDS board
-// buffer (dma_level_rolled) and each lane reads its rolled column pair from there at
-// two base addresses plus immediate row offsets, so that no gather addresses are held
-// and a board's rows and its planes are never live together.
+// wave_reset within the step kernel's register budget (k_env_reset_step_list, whose
+// waves must fit the step kernel's slots): the same result.  The level's goals, then
+// its board, are DMA'd row-rolled into the wave's LDS board buffer (dma_level_rolled)
+// and each lane reads its rolled column pair from there at two base addresses plus
+// immediate row offsets, so that no gather addresses are held and a board's rows and
+// its planes are never live together (75 VGPRs; wave_reset keeps every gather in
+// flight at once and takes 239).
 __device__ __forceinline__ void wave_reset_lean(const sl_env_state &st, const sl_level_pool &pool,
                                                 const ResetArgs &ra, int64_t b, int lane,
                                                 lds_u32 *buf) {
@@ -939,92 +886,19 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
         else
             sl::obs::obs_packed_wave(st, oa, b, lane, lfx.obs_out);
     }
-    if (fx.tail_workers) {
-        tail_publish(fx.scratch, st.B, a.step, b, reset, lane);
-    } else if (fx.fuse_reset && reset && lane == 0) {
-        // queue the env for the reset kernel (k_env_reset_list)
-        int64_t *cnt = fx.scratch + 8 * st.B + 2 + (a.step & 1);
+    if (fx.fuse_reset && reset && lane == 0) {
+        // queue the env for the reset kernel (k_env_reset_list); deferred, mark it too
+        // and list it in its step parity's own list (k_env_reset_step_list reads the
+        // last step's while this one fills)
+        int64_t *cnt = fx.defer_reset ? deferred_count(fx.scratch, st.B, a.step)
+                                      : fx.scratch + 8 * st.B + 2 + (a.step & 1);
         const int i = (int)atomicAdd((unsigned long long *)cnt, 1ull);
-        reset_list(fx.scratch)[i] = (int32_t)b;
-    }
-}
-
-// the view of a reset env, from its stored state (this wave's own stores, landed)
-__device__ __forceinline__ void reset_view(const FastExtra &fx, int64_t b, int lane, uint16_t *vm) {
-    wait_vm();
-    sl::obs::ObsArgs oa{};
-    oa.vh = fx.obs_vh;
-    oa.vw = fx.obs_vw;
-    oa.remove_white = fx.obs_rw;
-    oa.mode = fx.obs_mode;
-    oa.nch = fx.obs_nch;
-    const sl::obs::ChanMap cm{fx.obs_chpack, oa.nch};
-    uint8_t *o8 = reinterpret_cast<uint8_t *>(fx.obs_out);
-    if (oa.mode == SL_OBS_PACKED)
-        sl::obs::obs_packed_wave(st_of_kernarg(), oa, b, lane, fx.obs_out);
-    else if (oa.mode == SL_OBS_CHANNELS_U8)
-        sl::obs::obs_channels_wave<1>(st_of_kernarg(), oa, cm, fx.obs_one, b, lane, vm, o8);
-    else if (oa.mode == SL_OBS_CHANNELS_F32)
-        sl::obs::obs_channels_wave<4>(st_of_kernarg(), oa, cm, fx.obs_one, b, lane, vm, o8);
-    else
-        sl::obs::obs_channels_wave<2>(st_of_kernarg(), oa, cm, fx.obs_one, b, lane, vm, o8);
-}
-
-template <int OBS>
-__device__ __forceinline__ void tail_reset_one(int64_t b, int lane, lds_u32 *buf, uint16_t *vm) {
-    const StepKArgs &kb = kernarg();
-    wave_reset_lean(kb.st, kb.fx.pool, kb.fx.ra, b, lane, buf);
-    if (OBS) reset_view(kernarg().fx, b, lane, vm);
-}
-
-// A tail worker (workgroup B + w of the step launch): entries w, w + n, w + 2n, ...
-// of this step's list, each reset as k_env_reset_list does.
-template <int OBS>
-__device__ __forceinline__ void tail_worker(int w, int lane, lds_u32 *buf, uint16_t *vm) {
-    const StepKArgs &ka = kernarg();
-    const int64_t B = ka.st.B;
-    const uint32_t step = ka.a.step;
-    const TailWords tw = tail_words(ka.fx.scratch, B, step);
-    const int n = (int)gridDim.x - (int)B;
-    if (w == 0 && lane == 0) {      // the next step's counters
-        *tw.next_cnt = 0;
-#pragma unroll
-        for (int k = 0; k < kDoneShards; k++) tw.next_done[k] = 0;
-    }
-    int spins = kTailSpins;
-    for (int k = w;; k += n) {
-        bool have = false;
-        for (;;) {
-            if (__builtin_amdgcn_readfirstlane((int)ld_agent(tw.cnt)) > k) {
-                have = true;
-                break;
-            }
-            int64_t d = 0;
-#pragma unroll
-            for (int s = 0; s < kDoneShards; s++) d += ld_agent(&tw.done[s]);
-            if (__builtin_amdgcn_readfirstlane((int)d) >= B) {
-                have = __builtin_amdgcn_readfirstlane((int)ld_agent(tw.cnt)) > k;
-                break;
-            }
-            if (--spins < 0) break;
-            __builtin_amdgcn_s_sleep(16);
+        if (fx.defer_reset) {
+            st.planes_ok[b] = 64;       // (the reset rewrites the mirror bits)
+            reset_list(fx.scratch)[(a.step & 1) * st.B + i] = (int32_t)b;
+        } else {
+            reset_list(fx.scratch)[i] = (int32_t)b;
         }
-        uint64_t e = 0;
-        while (have) {
-            e = ld_agent(&tw.list[k]);
-            if ((uint32_t)__builtin_amdgcn_readfirstlane((int)(e >> 32)) == tail_tag(step)) break;
-            if (--spins < 0) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (spins < 0) {
-            if (lane == 0) atomicOr((unsigned long long *)tw.err, 4ull);
-            return;
-        }
-        if (!have) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        wait_vm();
-        const int64_t b = __builtin_amdgcn_readfirstlane((int)(uint32_t)e);
-        tail_reset_one<OBS>(b, lane, buf, vm);
     }
 }
 
@@ -1040,9 +914,16 @@ k_env_step_bits64(StepKArgs ka) {
     __shared__ __attribute__((aligned(16))) uint16_t vmask[OBS >= 2 ? sl::obs::kFusedChanCells : 2];
     __shared__ uint8_t rowlist[OBS ? 64 : 1];   // changed rows by rank (store_rows)
     lds_u32 *buf = (lds_u32 *)&stage[0];
-    if (b >= ka.st.B) {                    // a tail worker
-        tail_worker<OBS>((int)(b - ka.st.B), lane, buf, vmask);
-        return;
+    // deferred resets (sl_env_cfg.defer_resets, the view-less Philox form): an env the
+    // last step finished is marked (planes_ok bit 6) and listed; k_env_reset_step_list,
+    // on a second stream beside this launch, resets it and steps the new episode, so
+    // this wave leaves it alone.  (Tested before the env's loads are issued: tested
+    // after them, on the record, the early exit cost the rest of the kernel 65 spilled
+    // registers.)
+    if (OBS == 0 && MODE == SPAWN_PHILOX && ka.fx.defer_reset) {
+        // (block 0: the next step's list length, read by nobody during this step)
+        if (b == 0 && lane == 0) *deferred_count(ka.fx.scratch, ka.st.B, ka.a.step + 1u) = 0;
+        if (__builtin_amdgcn_readfirstlane(ka.st.planes_ok[b]) & 64) return;
     }
     Pre pre;
     issue_pre(ka.st, ka.actions, b, lane, pre);
@@ -1111,21 +992,18 @@ k_stream_prologue64(StepKArgs ka) {
 __global__ void __launch_bounds__(64)
 k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scratch,
                  uint32_t step, sl::obs::ObsArgs oa, uint64_t chpack, uint32_t one,
-                 uint16_t *obs_out) {
+                 uint16_t *obs_out, int deferred) {
     // channel views of the reset envs: their masks
     __shared__ __attribute__((aligned(16))) uint16_t vmask[sl::obs::kFusedChanCells];
     int64_t *cnt = scratch + 8 * st.B + 2;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        cnt[(step + 1) & 1] = 0;
-        // and the tail resets' done counters of that parity (a step with a capture runs
-        // this kernel between steps that use tail_worker)
-        for (int k = 0; k < kDoneShards; k++) cnt[2 + kDoneShards * ((step + 1) & 1) + k] = 0;
-    }
-    const int32_t *list = reset_list(scratch);
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(step + 1) & 1] = 0;
+    // a deferring step's list (sl_env_flush_resets): its own length word and half
+    const int32_t *list = reset_list(scratch) + (deferred ? (int64_t)(step & 1) * st.B : 0);
+    const int64_t *len = deferred ? deferred_count(scratch, st.B, step) : cnt + (step & 1);
     // the first entry is loaded together with the length (grid <= B <= list size; the
     // value is used only when the entry is in the list)
     const int first = list[blockIdx.x];
-    const int n = (int)__builtin_amdgcn_readfirstlane((int)cnt[step & 1]);
+    const int n = (int)__builtin_amdgcn_readfirstlane((int)*len);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int64_t b = __builtin_amdgcn_readfirstlane(i == (int)blockIdx.x ? first : list[i]);
         wave_reset(st, pool, ra, b, threadIdx.x);
@@ -1143,6 +1021,62 @@ k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scr
             else
                 sl::obs::obs_channels_wave<2>(st, oa, cm, one, b, threadIdx.x, vmask, o8);
         }
+    }
+}
+
+// The deferred resets of the last step, beside this step's k_env_step_bits64 (which
+// skips them): list entry i of the last step, if still marked (planes_ok bit 6; an
+// env reset by sl_env_flush_resets since is not), is reset by one wave (the result of
+// k_env_reset_list's wave_reset) and then takes this step (step_env, as the step
+// kernel's wave would).  The two launches touch disjoint envs, so they run on two
+// streams with no ordering between them.  The waves have the step kernel's register
+// budget, so that they fit the slots its waves leave, and the launch is issued first
+// on a high-priority stream; one entry per workgroup (a loop over entries spilled), the
+// entries past the grid go to k_env_reset_step_rest after it.
+template <bool REST>
+__device__ __forceinline__ void reset_step_entry(const StepKArgs &k, int i, lds_u32 *buf,
+                                                 uint16_t *vmask, uint8_t *rowlist) {
+    const uint32_t prev = k.a.step - 1u;
+    const int32_t *list = reset_list(k.fx.scratch) + (int64_t)(prev & 1u) * k.st.B;
+    const int64_t b = __builtin_amdgcn_readfirstlane(list[i]);
+    if (b < 0 || b >= k.st.B) return;                  // (a list is only ever env ids)
+    if (!(__builtin_amdgcn_readfirstlane(k.st.planes_ok[b]) & 64)) return;
+    if (REST) wave_reset(k.st, k.fx.pool, k.fx.ra, b, lane_now());
+    else wave_reset_lean(k.st, k.fx.pool, k.fx.ra, b, lane_now(), buf);
+    wait_vm();              // the new episode is in HBM before its step reads it
+    const StepKArgs &k2 = kernarg();
+    Pre pre;
+    issue_pre(k2.st, k2.actions, b, lane_now(), pre);
+    dma_board(k2.st.board + b * (int64_t)(N * N), buf, lane_now());
+    step_env<0, SPAWN_PHILOX>(k2.st, k2.a, k2.fx, b, lane_now(), buf, vmask, rowlist, k2.actions,
+                              k2.ctp, k2.ctc, k2.reward_out, k2.done_out, k2.flags_out,
+                              k2.ep_len_out, k2.ep_rew_out, pre);
+    wait_vm();              // (before the LDS buffer is reused)
+}
+
+__global__ void __launch_bounds__(64, kMinWaves)
+k_env_reset_step_list(StepKArgs ka) {
+    __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
+    __shared__ __attribute__((aligned(16))) uint16_t vmask[2];
+    __shared__ uint8_t rowlist[1];
+    const int n = (int)__builtin_amdgcn_readfirstlane(
+        (int)*deferred_count(ka.fx.scratch, ka.st.B, ka.a.step - 1u));
+    if ((int)blockIdx.x < n)
+        reset_step_entry<false>(kernarg(), blockIdx.x, (lds_u32 *)&stage[0], vmask, rowlist);
+}
+
+// the entries past k_env_reset_step_list's grid (more envs finished on one step than
+// it has workgroups): a loop over them, with a register budget of its own
+__global__ void __launch_bounds__(64)
+k_env_reset_step_rest(StepKArgs ka, int first) {
+    __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
+    __shared__ __attribute__((aligned(16))) uint16_t vmask[2];
+    __shared__ uint8_t rowlist[1];
+    const int n = (int)__builtin_amdgcn_readfirstlane(
+        (int)*deferred_count(ka.fx.scratch, ka.st.B, ka.a.step - 1u));
+    for (int i = first + (int)blockIdx.x; i < n; i += (int)gridDim.x) {
+        reset_step_entry<true>(kernarg(), i, (lds_u32 *)&stage[0], vmask, rowlist);
+        __builtin_amdgcn_s_barrier();
     }
 }
 
@@ -1176,12 +1110,8 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
     if (st.H != N || st.W != N) return SL_ETOOBIG;
-    // resets in the step launch's tail (tail_worker), unless a capture needs the frame
-    // between the step and its resets (then the reset-list kernel, as before)
-    StepKArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
-    ka.fx.tail_workers = (fx.fuse_reset && fx.pool.K > 0 && !fx.capture && st.B < (1ll << 31))
-                             ? kTailWorkers : 0;
     const unsigned grid = (unsigned)st.B;
+    const StepKArgs ka{st, a, fx, actions, ctp, ctc, reward, done, flags, ep_len, ep_rew};
     if (fx.obs_out && (fx.obs_vh < 1 || fx.obs_vw < 1 || fx.obs_vh * fx.obs_vw > 4096))
         return SL_EINVAL;
     if (fx.stream) {
@@ -1194,10 +1124,19 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         const int rc = stream_offsets(st, fx, s);
         if (rc || !stream_steps(fx)) return rc;
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        launch_bits64<SPAWN_STREAM>(obs_kind(fx), grid + ka.fx.tail_workers, ka, s);
+        launch_bits64<SPAWN_STREAM>(obs_kind(fx), grid, ka, s);
     } else {
+        if (fx.defer_reset && fx.side_stream) {
+            // the last step's deferred resets, on the side stream (sl_env_cfg.side_stream:
+            // ordered after this stream's work by the caller, and joined back by it)
+            hipStream_t ss = (hipStream_t)fx.side_stream;
+            const unsigned sg = (unsigned)(st.B < 512 ? st.B : 512);
+            hipLaunchKernelGGL(k_env_reset_step_list, dim3(sg), dim3(64), 0, ss, ka);
+            if (st.B > (int64_t)sg)
+                hipLaunchKernelGGL(k_env_reset_step_rest, dim3(64), dim3(64), 0, ss, ka, (int)sg);
+        }
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        launch_bits64<SPAWN_PHILOX>(obs_kind(fx), grid + ka.fx.tail_workers, ka, s);
+        launch_bits64<SPAWN_PHILOX>(obs_kind(fx), grid, ka, s);
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);
@@ -1205,7 +1144,7 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         const int rc = launch_capture(st, *fx.capture, flags, 0, s);
         if (rc) return rc;
     }
-    if (fx.fuse_reset && fx.pool.K > 0 && !ka.fx.tail_workers) {
+    if (fx.fuse_reset && fx.pool.K > 0 && !fx.defer_reset) {
         const unsigned grid = (unsigned)(st.B < 512 ? st.B : 512);
         sl::obs::ObsArgs oa{};
         oa.vh = fx.obs_vh;
@@ -1214,8 +1153,18 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         oa.mode = fx.obs_mode;
         oa.nch = fx.obs_nch;
         hipLaunchKernelGGL(k_env_reset_list, dim3(grid), dim3(64), 0, s, st, fx.pool, fx.ra,
-                           fx.scratch, a.step, oa, fx.obs_chpack, fx.obs_one, fx.obs_out);
+                           fx.scratch, a.step, oa, fx.obs_chpack, fx.obs_one, fx.obs_out, 0);
     }
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
+// the resets a deferring step left (sl_env_flush_resets): its reset-list kernel
+int launch_reset_list64(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
+                        int64_t *scratch, uint32_t step, hipStream_t s) {
+    if (st.H != N || st.W != N || pool.K < 1 || pool.H != N || pool.W != N) return SL_EINVAL;
+    const unsigned grid = (unsigned)(st.B < 512 ? st.B : 512);
+    hipLaunchKernelGGL(k_env_reset_list, dim3(grid), dim3(64), 0, s, st, pool, ra, scratch, step,
+                       sl::obs::ObsArgs{}, (uint64_t)0, 1u, (uint16_t *)nullptr, 1);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 

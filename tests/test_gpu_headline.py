@@ -194,16 +194,14 @@ def test_bench_regime_sampled_vs_oracle(torch_dev, pool_paths, obs):
             elif obs != "none":
                 assert np.array_equal(vo[e].cpu().numpy(), o), ctx
     assert n_reset >= 6
-    assert not venv.reset_error()
 
 
 @pytest.mark.parametrize("obs", ["none", "channels"])
-def test_mass_reset_in_step_tail(torch_dev, obs):
-    """Every env finishes on the same step: 8 192 resets in one launch, far more than
-    its tail workers (sl_bits.hip tail_worker: 64 workgroups, each looping over list
-    entries), with the rest of the batch still stepping beside them.  Sampled envs
-    bit-exact with the oracle over the reset and the steps after it; every env's
-    episode counter advanced exactly once."""
+def test_mass_reset_on_one_step(torch_dev, obs):
+    """Every env finishes on the same step: 8 192 resets in one reset-list launch (512
+    workgroups, each looping over list entries).  Sampled envs bit-exact with the
+    oracle over the reset and the steps after it; every env's episode counter
+    advanced."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
     levels = _levels(C3)
@@ -241,7 +239,6 @@ def test_mass_reset_in_step_tail(torch_dev, obs):
                 assert np.array_equal(vo[e].cpu().numpy(), o), ctx
         most = max(most, int(vd.sum()))
     assert most >= B * 9 // 10, most        # (nearly) every env timed out on one step
-    assert not venv.reset_error()
     n_ep = (venv.st_t["episodes"] - ep0).cpu().numpy()
     assert n_ep.min() >= 1 and n_ep.max() <= 2
 
