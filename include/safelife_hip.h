@@ -428,22 +428,6 @@ typedef struct sl_env_cfg {
                                        fills it for the step's range, so the
                                        stream is RandomState(seed) from
                                        *stream_pos on with no host buffer      */
-    int32_t defer_resets;           /* 64x64 boards, SL_RNG_PHILOX, auto_reset, no
-                                       obs_out, no capture: the envs a step
-                                       finishes are marked (planes_ok bit 6) and
-                                       listed, not reset.  The next sl_env_step
-                                       resets and steps them on side_stream while
-                                       its step kernel steps the rest on `stream`;
-                                       sl_env_flush_resets resets them now (call
-                                       it before reading their state).  Ignored
-                                       where the conditions do not hold.  The
-                                       results are those of an immediate reset.  */
-    void *side_stream;              /* hipStream_t for the last step's deferred
-                                       resets: required when the previous
-                                       sl_env_step deferred its resets (NULL
-                                       otherwise: nothing to launch).  The caller
-                                       orders it after `stream`'s prior work and
-                                       makes `stream` wait for it after the call */
 } sl_env_cfg;
 
 /*
@@ -462,16 +446,6 @@ int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const int32_t *acti
                 const sl_env_cfg *cfg, double *reward, uint8_t *done,
                 uint8_t *info_flags, int32_t *ep_len, int32_t *ep_reward,
                 void *stream);
-
-/*
- * The resets a step with cfg->defer_resets left pending: the envs step cfg->step
- * listed are reset from `pool` now (the reset-list kernel the step would have
- * launched).  Call at most once per deferring step, before the next step.
- * Replaces nothing in the reference (its resets are immediate, safelife_env.py:
- * 188-198); SL_EINVAL for boards other than 64x64.
- */
-int sl_env_flush_resets(sl_env_state *st, const sl_level_pool *pool, const sl_env_cfg *cfg,
-                        void *stream);
 
 /* Reset the envs with mask[b] != 0 (mask NULL = all) from `pool`. */
 int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const uint8_t *mask,

@@ -303,131 +303,6 @@ __device__ __forceinline__ void wave_reset(const sl_env_state &st, const sl_leve
     }
 }
 
-// A pool level into the wave's LDS board buffer with its rows rolled by dy: LDS row r
-// (128 bytes, columns unrolled, no chunk rotation) is level row (r - dy) & 63.  Each
-// DMA instruction fills 8 LDS rows; the roll is in the per-lane source addresses.
-__device__ __forceinline__ void dma_level_rolled(const uint16_t *__restrict__ src, lds_u32 *buf,
-                                                 int lane, int dy) {
-    const char *s = reinterpret_cast<const char *>(src);
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const int r = 8 * k + (lane >> 3);
-        __builtin_amdgcn_global_load_lds((const void *)(s + ((r - dy) & 63) * 128 + (lane & 7) * 16),
-                                         (__attribute__((address_space(3))) void *)(buf + k * 256),
-                                         16, 0, 0);
-    }
-}
-
-// wave_reset within the step kernel's register budget (k_env_reset_step_list, whose
-// waves must fit the step kernel's slots): the same result.  The level's goals, then
-// its board, are DMA'd row-rolled into the wave's LDS board buffer (dma_level_rolled)
-// and each lane reads its rolled column pair from there at two base addresses plus
-// immediate row offsets, so that no gather addresses are held and a board's rows and
-// its planes are never live together (75 VGPRs; wave_reset keeps every gather in
-// flight at once and takes 239).
-__device__ __forceinline__ void wave_reset_lean(const sl_env_state &st, const sl_level_pool &pool,
-                                                const ResetArgs &ra, int64_t b, int lane,
-                                                lds_u32 *buf) {
-    const int ep = __builtin_amdgcn_readfirstlane(st.episodes[b]);
-    const LevelChoice lc = choose_level_wave(pool, ra, ra.env0 + (uint32_t)b, ep, N, N, lane);
-    const int li = __builtin_amdgcn_readfirstlane(lc.idx);
-    const int dy = __builtin_amdgcn_readfirstlane(lc.dy), dx = __builtin_amdgcn_readfirstlane(lc.dx);
-    const LevelScalars ls = level_scalars(pool, li);
-    const int h = lane & 1, j = lane >> 1;
-    const uint16_t *lb = pool.board + (int64_t)li * (N * N), *lg = pool.goals + (int64_t)li * (N * N);
-    const int c0 = (2 * j - dx) & 63, c1 = (2 * j + 1 - dx) & 63;
-    const int64_t off = b * (int64_t)(N * N);
-    const uint32_t lane_off = (uint32_t)(h * 1024 + j);
-    u32 *gs = reinterpret_cast<u32 *>(st.start_board + off);
-    u32 *gg = reinterpret_cast<u32 *>(st.goals + off);
-    u32 *gb = reinterpret_cast<u32 *>(st.board + off);
-    typedef __attribute__((address_space(3))) const uint16_t lds_cu16_t;
-    lds_cu16_t *q0 = reinterpret_cast<lds_cu16_t *>(buf) + 32 * h * N + c0;
-    lds_cu16_t *q1 = reinterpret_cast<lds_cu16_t *>(buf) + 32 * h * N + c1;
-    auto rolled = [&](u32 D[32]) {
-#pragma unroll
-        for (int y = 0; y < 32; y++) D[y] = (u32)q0[y * N] | ((u32)q1[y * N] << 16);
-    };
-    dma_level_rolled(lg, buf, lane, dy);
-    wait_vm();
-    u32 P[32];
-    rolled(P);
-    wait_lgkm();                    // the goals are read out of the buffer
-    dma_level_rolled(lb, buf, lane, dy);    // under the goals' stores and sums
-#pragma unroll
-    for (int y = 0; y < 32; y++) gg[lane_off + y * 32] = P[y];
-    transpose32(P);
-    if (st.planes) {
-        u32 *mg = st.planes + b * 4096 + 2048;
-#pragma unroll
-        for (int q = 0; q < 32; q++) mg[(uint32_t)(q * 64 + lane)] = P[q];
-    }
-    u32 gcol[3][2];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        gcol[k][0] = PL(P, 9 + k, 0);
-        gcol[k][1] = PL(P, 9 + k, 1);
-    }
-    const bool sg = __ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull;
-    wait_vm();
-    rolled(P);
-#pragma unroll
-    for (int y = 0; y < 32; y++) gs[lane_off + y * 32] = P[y];
-    transpose32(P);
-    int pts, scr, pos, side;
-    score_planes(P, gcol, P, &pts, &scr, &pos, &side);
-    const int s1 = wave_total((pts + 192) | ((scr + 64) << 16));
-    const int s2 = wave_total(pos);
-    const bool sb = __ballot((PL(P, 7, 0) | PL(P, 7, 1)) != 0u) != 0ull;
-    const u32 ex0 = PL(P, 8, 0), ex1 = PL(P, 8, 1);
-    int ev = 0;
-    if (lane == 0)
-        ev = reset_scalars_from(st, ra, b, li, dy, dx, ls, ep, (s1 & 0xFFFF) - 192 * 64,
-                                ((s1 >> 16) & 0xFFFF) - 64 * 64, s2, (sb ? 1 : 0) | (sg ? 2 : 0));
-    ev = __builtin_amdgcn_readfirstlane(ev);
-    asm volatile("" ::: "memory");  // read the rows again (not kept through the sums)
-    rolled(P);
-#pragma unroll
-    for (int y = 0; y < 32; y++) {
-        u32 d = P[y];
-        if (d & (u32)EXIT) d = (d & 0xFFFF0000u) | (u32)ev;
-        if (d & ((u32)EXIT << 16)) d = (d & 0x0000FFFFu) | ((u32)ev << 16);
-        gb[lane_off + y * 32] = d;
-    }
-    const int n_exit = wave_total(__builtin_popcount(ex0) + __builtin_popcount(ex1));
-    {
-        u32 e0 = ex0, e1 = ex1;
-        const int kmax = n_exit < SL_MAX_EXITS ? n_exit : SL_MAX_EXITS;
-        for (int k = 0; k < kmax; k++) {
-            const u32 k0 = e0 ? (u32)((32 * h + __builtin_ctz(e0)) * N + 2 * j) : 0xFFFFu;
-            const u32 k1 = e1 ? (u32)((32 * h + __builtin_ctz(e1)) * N + 2 * j + 1) : 0xFFFFu;
-            u32 m = k0 < k1 ? k0 : k1;
-            m = min(m, dpp<0xB1>(m));
-            m = min(m, dpp<0x4E>(m));
-            m = min(m, dpp<0x141>(m));
-            m = min(m, dpp<0x140>(m));
-            const u32 key = min(min((u32)__builtin_amdgcn_readlane((int)m, 0),
-                                    (u32)__builtin_amdgcn_readlane((int)m, 16)),
-                                min((u32)__builtin_amdgcn_readlane((int)m, 32),
-                                    (u32)__builtin_amdgcn_readlane((int)m, 48)));
-            if (k0 == key) e0 &= e0 - 1;
-            if (k1 == key) e1 &= e1 - 1;
-            if (lane == 0) {
-                st.exit_y[b * SL_MAX_EXITS + k] = (int16_t)(key >> 6);
-                st.exit_x[b * SL_MAX_EXITS + k] = (int16_t)(key & 63);
-            }
-        }
-    }
-    if (lane == 0) {
-        if (st.planes) st.planes_ok[b] = 2;
-        st.exit_count[b] = n_exit;
-        for (int e = n_exit; e < SL_MAX_EXITS; e++) {
-            st.exit_y[b * SL_MAX_EXITS + e] = 0;
-            st.exit_x[b * SL_MAX_EXITS + e] = 0;
-        }
-    }
-}
-
 // all kernel arguments of k_env_step_bits64 in one struct at kernarg offset 0, so a
 // phase can re-read one late through kernarg() (write_obs)
 struct StepKArgs {
@@ -449,7 +324,6 @@ __device__ __forceinline__ const StepKArgs &kernarg() {
     asm volatile("" : "+s"(kp));
     return *(const StepKArgs *)kp;
 }
-__device__ __forceinline__ const sl_env_state &st_of_kernarg() { return kernarg().st; }
 
 // ---------------------------------------------------------------- fused observation
 // SafeLifeEnv.get_obs + recenter_view (safelife_env.py:125-155, helper_utils.py:41-74)
@@ -887,25 +761,17 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
             sl::obs::obs_packed_wave(st, oa, b, lane, lfx.obs_out);
     }
     if (fx.fuse_reset && reset && lane == 0) {
-        // queue the env for the reset kernel (k_env_reset_list); deferred, mark it too
-        // and list it in its step parity's own list (k_env_reset_step_list reads the
-        // last step's while this one fills)
-        int64_t *cnt = fx.defer_reset ? deferred_count(fx.scratch, st.B, a.step)
-                                      : fx.scratch + 8 * st.B + 2 + (a.step & 1);
+        // queue the env for the reset kernel (k_env_reset_list)
+        int64_t *cnt = fx.scratch + 8 * st.B + 2 + (a.step & 1);
         const int i = (int)atomicAdd((unsigned long long *)cnt, 1ull);
-        if (fx.defer_reset) {
-            st.planes_ok[b] = 64;       // (the reset rewrites the mirror bits)
-            reset_list(fx.scratch)[(a.step & 1) * st.B + i] = (int32_t)b;
-        } else {
-            reset_list(fx.scratch)[i] = (int32_t)b;
-        }
+        reset_list(fx.scratch)[i] = (int32_t)b;
     }
 }
 
 // OBS: also write the observation (fx.obs_out): 1 packed, 2-4 channel views
 // (obs_esz); MODE: see step_env
 template <int OBS, int MODE>
-__global__ void __launch_bounds__(64, MODE == SPAWN_STREAM ? kMinWavesObs : kMinWaves)
+__global__ void __launch_bounds__(64, (OBS || MODE == SPAWN_STREAM) ? kMinWavesObs : kMinWaves)
 k_env_step_bits64(StepKArgs ka) {
     const int64_t b = blockIdx.x;          // one wave per env
     const int lane = threadIdx.x;
@@ -914,17 +780,6 @@ k_env_step_bits64(StepKArgs ka) {
     __shared__ __attribute__((aligned(16))) uint16_t vmask[OBS >= 2 ? sl::obs::kFusedChanCells : 2];
     __shared__ uint8_t rowlist[OBS ? 64 : 1];   // changed rows by rank (store_rows)
     lds_u32 *buf = (lds_u32 *)&stage[0];
-    // deferred resets (sl_env_cfg.defer_resets, the view-less Philox form): an env the
-    // last step finished is marked (planes_ok bit 6) and listed; k_env_reset_step_list,
-    // on a second stream beside this launch, resets it and steps the new episode, so
-    // this wave leaves it alone.  (Tested before the env's loads are issued: tested
-    // after them, on the record, the early exit cost the rest of the kernel 65 spilled
-    // registers.)
-    if (OBS == 0 && MODE == SPAWN_PHILOX && ka.fx.defer_reset) {
-        // (block 0: the next step's list length, read by nobody during this step)
-        if (b == 0 && lane == 0) *deferred_count(ka.fx.scratch, ka.st.B, ka.a.step + 1u) = 0;
-        if (__builtin_amdgcn_readfirstlane(ka.st.planes_ok[b]) & 64) return;
-    }
     Pre pre;
     issue_pre(ka.st, ka.actions, b, lane, pre);
     dma_board(ka.st.board + b * (int64_t)(N * N), buf, lane);
@@ -992,18 +847,16 @@ k_stream_prologue64(StepKArgs ka) {
 __global__ void __launch_bounds__(64)
 k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scratch,
                  uint32_t step, sl::obs::ObsArgs oa, uint64_t chpack, uint32_t one,
-                 uint16_t *obs_out, int deferred) {
+                 uint16_t *obs_out) {
     // channel views of the reset envs: their masks
     __shared__ __attribute__((aligned(16))) uint16_t vmask[sl::obs::kFusedChanCells];
     int64_t *cnt = scratch + 8 * st.B + 2;
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(step + 1) & 1] = 0;
-    // a deferring step's list (sl_env_flush_resets): its own length word and half
-    const int32_t *list = reset_list(scratch) + (deferred ? (int64_t)(step & 1) * st.B : 0);
-    const int64_t *len = deferred ? deferred_count(scratch, st.B, step) : cnt + (step & 1);
+    const int32_t *list = reset_list(scratch);
     // the first entry is loaded together with the length (grid <= B <= list size; the
     // value is used only when the entry is in the list)
     const int first = list[blockIdx.x];
-    const int n = (int)__builtin_amdgcn_readfirstlane((int)*len);
+    const int n = (int)__builtin_amdgcn_readfirstlane((int)cnt[step & 1]);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int64_t b = __builtin_amdgcn_readfirstlane(i == (int)blockIdx.x ? first : list[i]);
         wave_reset(st, pool, ra, b, threadIdx.x);
@@ -1021,62 +874,6 @@ k_env_reset_list(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t *scr
             else
                 sl::obs::obs_channels_wave<2>(st, oa, cm, one, b, threadIdx.x, vmask, o8);
         }
-    }
-}
-
-// The deferred resets of the last step, beside this step's k_env_step_bits64 (which
-// skips them): list entry i of the last step, if still marked (planes_ok bit 6; an
-// env reset by sl_env_flush_resets since is not), is reset by one wave (the result of
-// k_env_reset_list's wave_reset) and then takes this step (step_env, as the step
-// kernel's wave would).  The two launches touch disjoint envs, so they run on two
-// streams with no ordering between them.  The waves have the step kernel's register
-// budget, so that they fit the slots its waves leave, and the launch is issued first
-// on a high-priority stream; one entry per workgroup (a loop over entries spilled), the
-// entries past the grid go to k_env_reset_step_rest after it.
-template <bool REST>
-__device__ __forceinline__ void reset_step_entry(const StepKArgs &k, int i, lds_u32 *buf,
-                                                 uint16_t *vmask, uint8_t *rowlist) {
-    const uint32_t prev = k.a.step - 1u;
-    const int32_t *list = reset_list(k.fx.scratch) + (int64_t)(prev & 1u) * k.st.B;
-    const int64_t b = __builtin_amdgcn_readfirstlane(list[i]);
-    if (b < 0 || b >= k.st.B) return;                  // (a list is only ever env ids)
-    if (!(__builtin_amdgcn_readfirstlane(k.st.planes_ok[b]) & 64)) return;
-    if (REST) wave_reset(k.st, k.fx.pool, k.fx.ra, b, lane_now());
-    else wave_reset_lean(k.st, k.fx.pool, k.fx.ra, b, lane_now(), buf);
-    wait_vm();              // the new episode is in HBM before its step reads it
-    const StepKArgs &k2 = kernarg();
-    Pre pre;
-    issue_pre(k2.st, k2.actions, b, lane_now(), pre);
-    dma_board(k2.st.board + b * (int64_t)(N * N), buf, lane_now());
-    step_env<0, SPAWN_PHILOX>(k2.st, k2.a, k2.fx, b, lane_now(), buf, vmask, rowlist, k2.actions,
-                              k2.ctp, k2.ctc, k2.reward_out, k2.done_out, k2.flags_out,
-                              k2.ep_len_out, k2.ep_rew_out, pre);
-    wait_vm();              // (before the LDS buffer is reused)
-}
-
-__global__ void __launch_bounds__(64, kMinWaves)
-k_env_reset_step_list(StepKArgs ka) {
-    __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
-    __shared__ __attribute__((aligned(16))) uint16_t vmask[2];
-    __shared__ uint8_t rowlist[1];
-    const int n = (int)__builtin_amdgcn_readfirstlane(
-        (int)*deferred_count(ka.fx.scratch, ka.st.B, ka.a.step - 1u));
-    if ((int)blockIdx.x < n)
-        reset_step_entry<false>(kernarg(), blockIdx.x, (lds_u32 *)&stage[0], vmask, rowlist);
-}
-
-// the entries past k_env_reset_step_list's grid (more envs finished on one step than
-// it has workgroups): a loop over them, with a register budget of its own
-__global__ void __launch_bounds__(64)
-k_env_reset_step_rest(StepKArgs ka, int first) {
-    __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
-    __shared__ __attribute__((aligned(16))) uint16_t vmask[2];
-    __shared__ uint8_t rowlist[1];
-    const int n = (int)__builtin_amdgcn_readfirstlane(
-        (int)*deferred_count(ka.fx.scratch, ka.st.B, ka.a.step - 1u));
-    for (int i = first + (int)blockIdx.x; i < n; i += (int)gridDim.x) {
-        reset_step_entry<true>(kernarg(), i, (lds_u32 *)&stage[0], vmask, rowlist);
-        __builtin_amdgcn_s_barrier();
     }
 }
 
@@ -1126,15 +923,6 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
         launch_bits64<SPAWN_STREAM>(obs_kind(fx), grid, ka, s);
     } else {
-        if (fx.defer_reset && fx.side_stream) {
-            // the last step's deferred resets, on the side stream (sl_env_cfg.side_stream:
-            // ordered after this stream's work by the caller, and joined back by it)
-            hipStream_t ss = (hipStream_t)fx.side_stream;
-            const unsigned sg = (unsigned)(st.B < 512 ? st.B : 512);
-            hipLaunchKernelGGL(k_env_reset_step_list, dim3(sg), dim3(64), 0, ss, ka);
-            if (st.B > (int64_t)sg)
-                hipLaunchKernelGGL(k_env_reset_step_rest, dim3(64), dim3(64), 0, ss, ka, (int)sg);
-        }
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
         launch_bits64<SPAWN_PHILOX>(obs_kind(fx), grid, ka, s);
     }
@@ -1144,7 +932,7 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         const int rc = launch_capture(st, *fx.capture, flags, 0, s);
         if (rc) return rc;
     }
-    if (fx.fuse_reset && fx.pool.K > 0 && !fx.defer_reset) {
+    if (fx.fuse_reset && fx.pool.K > 0) {
         const unsigned grid = (unsigned)(st.B < 512 ? st.B : 512);
         sl::obs::ObsArgs oa{};
         oa.vh = fx.obs_vh;
@@ -1153,18 +941,8 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         oa.mode = fx.obs_mode;
         oa.nch = fx.obs_nch;
         hipLaunchKernelGGL(k_env_reset_list, dim3(grid), dim3(64), 0, s, st, fx.pool, fx.ra,
-                           fx.scratch, a.step, oa, fx.obs_chpack, fx.obs_one, fx.obs_out, 0);
+                           fx.scratch, a.step, oa, fx.obs_chpack, fx.obs_one, fx.obs_out);
     }
-    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
-}
-
-// the resets a deferring step left (sl_env_flush_resets): its reset-list kernel
-int launch_reset_list64(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
-                        int64_t *scratch, uint32_t step, hipStream_t s) {
-    if (st.H != N || st.W != N || pool.K < 1 || pool.H != N || pool.W != N) return SL_EINVAL;
-    const unsigned grid = (unsigned)(st.B < 512 ? st.B : 512);
-    hipLaunchKernelGGL(k_env_reset_list, dim3(grid), dim3(64), 0, s, st, pool, ra, scratch, step,
-                       sl::obs::ObsArgs{}, (uint64_t)0, 1u, (uint16_t *)nullptr, 1);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 

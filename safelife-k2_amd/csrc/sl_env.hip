@@ -1038,16 +1038,6 @@ extern "C" int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const u
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
-extern "C" int sl_env_flush_resets(sl_env_state *st, const sl_level_pool *pool,
-                                   const sl_env_cfg *cfg, void *stream) {
-    if (!state_ok(st) || !pool || !cfg || !cfg->scratch || pool->K <= 0 || pool->H != st->H ||
-        pool->W != st->W)
-        return SL_EINVAL;
-    if (st->B == 0) return SL_OK;
-    return launch_reset_list64(*st, *pool, reset_args(cfg), cfg->scratch, cfg->step,
-                               (hipStream_t)stream);
-}
-
 extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const int32_t *actions,
                            const sl_env_cfg *cfg, double *reward, uint8_t *done,
                            uint8_t *info_flags, int32_t *ep_len, int32_t *ep_reward,
@@ -1119,11 +1109,6 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     // their reset-list kernel, so they keep the list (and its per-parity lengths,
     // which only the reset-list kernel clears) going through captured steps.
     if (cap && small) fx.fuse_reset = 0;
-    // deferred resets: the 64x64 Philox kernel without views or capture
-    fx.defer_reset = (cfg->defer_resets && fast && !replay && !cap && !cfg->obs_out &&
-                      fx.fuse_reset && pool && pool->K > 0 && pool->H == 64 && pool->W == 64 &&
-                      st->planes && st->planes_ok) ? 1 : 0;
-    fx.side_stream = cfg->side_stream;
     // observations: packed views of 64x64 boards come out of the step kernel itself
     ObsArgs oa;
     if (cfg->obs_out) {

@@ -18,9 +18,6 @@ namespace sl {
 //   [8B]      error flags (bit0: draw stream exhausted)
 //   [8B+2], [8B+3]  reset-list lengths for even / odd steps (each step's reset
 //             kernel zeroes the other one)
-//   [8B+4, 8B+8)  a 64x64 step that defers its resets (FastExtra::defer_reset): the
-//             list length of step t at [8B+4 + t % 4] (deferred_count), the list at
-//             int32 offset (t & 1) * B
 struct Scratch {
     int64_t *counts, *offsets, *act, *err;
 };
@@ -28,12 +25,6 @@ __host__ __device__ inline Scratch scratch_of(int64_t *s, int64_t B) {
     return Scratch{s, s + 2 * B, s + 4 * B, s + 8 * B};
 }
 __host__ __device__ inline int32_t *reset_list(int64_t *s) { return reinterpret_cast<int32_t *>(s); }
-// the list length of deferring step `step` (scratch[8B+4 + step % 4]): step t fills its
-// own, the next step's side-stream kernel reads it while that step fills another, and
-// each deferring step's kernel clears the one step t + 1 will fill
-__host__ __device__ inline int64_t *deferred_count(int64_t *s, int64_t B, uint32_t step) {
-    return s + 8 * B + 4 + (step & 3u);
-}
 
 // the board planes a cell's spawn eligibility reads (alive, frozen, inhibiting,
 // spawning): what the 128x128 replay paths evaluate eligibility from
@@ -341,11 +332,6 @@ struct FastExtra {
     const int64_t *stream_base;   // *stream_base + the step
     const sl_mt19937 *mt;   // replay from the device generator (sl_env_cfg.mt) or NULL:
                             // stream_offsets fills its ring for the step's range
-    int32_t defer_reset = 0;    // 64x64 Philox, no views: finished envs are marked
-                                // (planes_ok bit 6) and listed per step parity; the next
-                                // step resets and steps them on side_stream
-                                // (k_env_reset_step_list), or sl_env_flush_resets
-    void *side_stream = nullptr;
 };
 // replay-mode phases of a bit-sliced launcher: whether it runs the action + count
 // prologue, and whether it continues past the offsets scan to the step kernel
@@ -379,9 +365,6 @@ int launch_env_action(const sl_env_state &st, const int32_t *actions, int ctp, i
 // block each (sl_env.hip)
 int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
                            int64_t *scratch, uint32_t step, hipStream_t s);
-// the reset-list kernel of a 64x64 step that deferred its resets (sl_bits.hip)
-int launch_reset_list64(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
-                        int64_t *scratch, uint32_t step, hipStream_t s);
 // bit-sliced 64x64 kernel (sl_bits.hip)
 int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,

@@ -64,8 +64,7 @@ class EnvCfg(ctypes.Structure):
                 ("ev_begin", vp), ("ev_end", vp), ("kernel", i32),
                 ("obs_out", vp), ("obs_mode", i32), ("obs_vh", i32), ("obs_vw", i32),
                 ("obs_remove_white", i32), ("obs_nch", i32), ("obs_channels", i32 * 16),
-                ("capture", vp), ("stream_phase", i32), ("stream_base", vp), ("mt", vp),
-                ("defer_resets", i32), ("side_stream", vp)]
+                ("capture", vp), ("stream_phase", i32), ("stream_base", vp), ("mt", vp)]
 
 
 class MT19937(ctypes.Structure):
@@ -114,8 +113,6 @@ def lib():
                               ctypes.POINTER(EnvCfg), vp, vp, vp, vp, vp, vp]
     L.sl_env_reset.argtypes = [ctypes.POINTER(EnvState), ctypes.POINTER(LevelPool), vp,
                                ctypes.POINTER(EnvCfg), vp]
-    L.sl_env_flush_resets.argtypes = [ctypes.POINTER(EnvState), ctypes.POINTER(LevelPool),
-                                      ctypes.POINTER(EnvCfg), vp]
     L.sl_level_pool_prepare.argtypes = [ctypes.POINTER(LevelPool), vp]
     L.sl_side_effect_workspace.argtypes = [i64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64)]
     L.sl_side_effect_densities.argtypes = [vp, vp, vp, vp, vp, i64, ctypes.c_int, ctypes.c_int,

@@ -73,8 +73,7 @@ class SafeLifeVecEnv:
                  auto_reset=True, rng="philox", seed=0, spawn_stream=None,
                  level_order="sequential", augment_roll=False, env0=0, n_total_envs=None,
                  can_toggle_powers=False, can_toggle_colors=False, obs_dtype="uint16",
-                 compute_obs=True, global_counter=None, kernel="auto", stream_exchange=None,
-                 defer_resets=True):
+                 compute_obs=True, global_counter=None, kernel="auto", stream_exchange=None):
         import torch
         self.torch = torch
         self.device = _lib.require_device(device)
@@ -109,12 +108,6 @@ class SafeLifeVecEnv:
         # contract) places this shard's draws in the global stream every step
         self.stream_exchange = stream_exchange
         self._step_index = 0
-        # resets of finished envs deferred to the next step's kernel when nothing reads
-        # the state in between (64x64, Philox, no views): the step index whose resets
-        # are pending, or None (_flush_resets)
-        self.defer_resets = bool(defer_resets)
-        self._pending_reset = None
-        self._side = None
         # step index and auto_reset flag of the last launched step: the 64x64 and
         # 128x128 kernels queue finished envs in per-parity lists (sl_env_cfg.scratch)
         # that are valid only for consecutive auto-reset steps
@@ -153,53 +146,14 @@ class SafeLifeVecEnv:
             raise ValueError("rng must be 'philox' or 'stream'")
         self._bonus_key = None
 
-    # ------------------------------------------------------------ state tensors
-    # The per-env state lives in these device tensors.  With deferred resets (a 64x64
-    # Philox step without views: sl_env_cfg.defer_resets) the envs a step finished are
-    # reset by the next step's kernel, before it steps them; reading any of these first
-    # launches their resets (sl_env_flush_resets, stream-ordered), so what a reader
-    # sees is always the state after the step's resets.
-    def _state_view(name, doc):
-        def get(self):
-            self._flush_resets()
-            return self.__dict__["_" + name]
-        return property(get, doc=doc)
-
-    board = _state_view("board", "uint16 [B, H, W] cells (safelife_game.py board)")
-    goals = _state_view("goals", "uint16 [B, H, W] goal cells")
-    start_board = _state_view("start_board", "uint16 [B, H, W] the episode's first board")
-    st_t = _state_view("st_t", "dict of the per-env scalar state tensors")
-    planes = _state_view("planes", "the bit-sliced kernels' goal-plane mirror (derived)")
-    planes_ok = _state_view("planes_ok", "int32 [B] validity bits of `planes` (derived)")
-    del _state_view
-
-    def _flush_resets(self):
-        """Launch the resets the last step deferred (no-op when none are pending)."""
-        step = self.__dict__.get("_pending_reset")
-        if step is None:
-            return
-        self._pending_reset = None
-        cfg = _lib.EnvCfg()          # a copy: a step may be filling self._cfg
-        ctypes.memmove(ctypes.byref(cfg), ctypes.byref(self._fill_cfg()), ctypes.sizeof(cfg))
-        cfg.step = step & 0xFFFFFFFF
-        _lib.check(_lib.lib().sl_env_flush_resets(
-            ctypes.byref(self._state), ctypes.byref(self._pool_dev["struct"]), ctypes.byref(cfg),
-            _lib.stream_ptr(self.device)), "sl_env_flush_resets")
-
-    def _defers(self, cfg, obs):
-        """Does sl_env_step defer this step's resets (sl_env_step's own condition)?"""
-        return (self.defer_resets and self.auto_reset and obs is None and cfg.capture is None
-                and cfg.rng_mode == _lib.SL_RNG_PHILOX and (self.H, self.W) == (64, 64)
-                and self.kernel != _lib.SL_KERNEL_GENERIC)
-
     # ------------------------------------------------------------------ setup
     def _alloc(self, obs_dtype):
         torch, dev, B, H, W = self.torch, self.device, self.B, self.H, self.W
         z = lambda *s, dt=torch.int32: torch.zeros(s, dtype=dt, device=dev)
-        self._board = z(B, H, W, dt=torch.uint16)
-        self._goals = z(B, H, W, dt=torch.uint16)
-        self._start_board = z(B, H, W, dt=torch.uint16)
-        self._st_t = {
+        self.board = z(B, H, W, dt=torch.uint16)
+        self.goals = z(B, H, W, dt=torch.uint16)
+        self.start_board = z(B, H, W, dt=torch.uint16)
+        self.st_t = {
             "agent_x": z(B), "agent_y": z(B), "orientation": z(B), "game_over": z(B),
             "episode_length": z(B), "episode_reward": z(B), "old_points": z(B),
             "baseline": z(B), "score": z(B), "possible": z(B), "side_effect": z(B),
@@ -214,17 +168,17 @@ class SafeLifeVecEnv:
         }
         s = _lib.EnvState()
         s.B, s.H, s.W = B, H, W
-        s.board, s.goals, s.start_board = (self._board.data_ptr(), self._goals.data_ptr(),
-                                           self._start_board.data_ptr())
-        for k, t in self._st_t.items():
+        s.board, s.goals, s.start_board = (self.board.data_ptr(), self.goals.data_ptr(),
+                                           self.start_board.data_ptr())
+        for k, t in self.st_t.items():
             setattr(s, k, t.data_ptr())
         # bit-plane mirror of the goals kept by the bit-sliced kernels (derived data):
         # 64x64 [B, 2, 32, 64] (half 1 = goals), 128x128 [B, 4 bands, 32, 64]
-        self._planes_ok = z(B)
+        self.planes_ok = z(B)
         if (H, W) in ((64, 64), (128, 128)):
-            self._planes = z(B, H // 32, 32, 64)
-            s.planes = self._planes.data_ptr()
-            s.planes_ok = self._planes_ok.data_ptr()
+            self.planes = z(B, H // 32, 32, 64)
+            s.planes = self.planes.data_ptr()
+            s.planes_ok = self.planes_ok.data_ptr()
         if (H, W) == (128, 128) and self.rng == "stream":
             # replay's draw planes: each tensor's eligible cells, then its decided
             # spawns (4 KiB per env)
@@ -357,7 +311,6 @@ class SafeLifeVecEnv:
     # -------------------------------------------------------------- gym-ish API
     def reset(self, mask=None):
         """Reset all envs (or those with mask[b] != 0); returns observations."""
-        self._flush_resets()
         L = _lib.lib()
         cfg = self._fill_cfg()
         m = None
@@ -411,7 +364,6 @@ class SafeLifeVecEnv:
         ch = self._channels if self.obs_mode != _lib.SL_OBS_PACKED else None
         nch = len(self.output_channels) if self.output_channels else 0
         out = self.obs if out is None else self._obs_target(out)
-        self._flush_resets()
         _lib.check(L.sl_env_obs(ctypes.byref(self._state), vh, vw, int(self.remove_white_goals),
                                 self.obs_mode, ch, nch, out.data_ptr(),
                                 _lib.stream_ptr(self.device)), "sl_env_obs")
@@ -446,6 +398,7 @@ class SafeLifeVecEnv:
         self._actions_in_flight = a
         L = _lib.lib()
         cfg = self._fill_cfg()
+        self._check_reset_lists()
         cfg.capture = self._recorder._next_capture() if self._recorder is not None else None
         # the observation is written by sl_env_step itself (from the on-chip board
         # where the kernel allows it)
@@ -453,23 +406,6 @@ class SafeLifeVecEnv:
         if self.compute_obs or obs_out is not None:
             obs = self.obs if obs_out is None else self._obs_target(obs_out)
         self._fill_obs_cfg(cfg, obs)
-        defer = self._defers(cfg, obs)
-        if not defer:
-            self._flush_resets()
-        self._check_reset_lists(defer)
-        cfg.defer_resets = int(defer)
-        # deferred resets of the last step: reset and stepped on a side stream beside this
-        # step's kernel (sl_env_cfg.side_stream), ordered after this stream's work so far
-        # and joined back after the launch
-        side = None
-        cfg.side_stream = None
-        if defer and self._pending_reset is not None:
-            if self._side is None:
-                # high priority: its few waves are dispatched ahead of the step kernel's
-                self._side = torch.cuda.Stream(device=self.device, priority=-1)
-            side = self._side
-            side.wait_stream(torch.cuda.current_stream(self.device))
-            cfg.side_stream = side.cuda_stream
         outs = [self._out(reward_out, self.reward), self._out(done_out, self.done),
                 self._out(flags_out, self.flags), self._out(ep_len_out, self.ep_len),
                 self._out(ep_rew_out, self.ep_rew)]
@@ -487,23 +423,18 @@ class SafeLifeVecEnv:
             cfg.stream_phase = 2
             cfg.stream_base = self._stream_base.data_ptr()
         launch()
-        if side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(side)
-        self._pending_reset = self._step_index if defer else None
         self._step_index += 1
         self.global_counter.num_steps += self.B
 
-    def _check_reset_lists(self, defer=False):
+    def _check_reset_lists(self):
         """Zero the per-parity reset-list lengths (scratch[8B+2 : 8B+4]) unless this
-        step directly follows an auto-reset step of the same kind (resets deferred or
-        not): each step's reset kernel -- or, deferred, the next step's side-stream
-        kernel -- clears only the list it has consumed (sl_env_common.h, Scratch)."""
-        cur = (self._step_index, self.auto_reset, bool(defer))
+        step directly follows an auto-reset step: each step's reset kernel zeroes
+        only the other parity's list (sl_env_common.h, Scratch)."""
+        cur = (self._step_index, self.auto_reset)
         last = self._last_step
-        if not (self.auto_reset and last is not None and last[1] and last[2] == bool(defer)
+        if not (self.auto_reset and last is not None and last[1]
                 and last[0] + 1 == self._step_index):
-            # (and the deferring steps' four list lengths, deferred_count)
-            self.scratch[8 * self.B + 2:8 * self.B + 8].zero_()
+            self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()
         self._last_step = cur
 
     def _fill_obs_cfg(self, cfg, out):
@@ -545,7 +476,6 @@ class SafeLifeVecEnv:
         pointer offset by i0 envs (the C ABI's slicing convention), for the
         game-level entry points (sl_env_action / _advance / _rescore /
         _exit_colors) on part of the batch."""
-        self._flush_resets()
         if not (0 <= i0 and n >= 0 and i0 + n <= self.B):
             raise IndexError("env slice [%d, %d) outside [0, %d)" % (i0, i0 + n, self.B))
         full, s = self._state, _lib.EnvState()
@@ -576,7 +506,6 @@ class SafeLifeVecEnv:
 
     def set_state(self, board, goals, start_board, **scalars):
         """Load explicit state (for tests / checkpoints).  Arrays are [B,...]."""
-        self._flush_resets()
         torch = self.torch
         for dst, src in ((self.board, board), (self.goals, goals), (self.start_board, start_board)):
             dst.copy_(torch.as_tensor(np.ascontiguousarray(src, dtype=np.uint16)).to(self.device))
@@ -596,7 +525,7 @@ class SafeLifeVecEnv:
         self.st_t["spawn_flags"].copy_(3 | 4 * hi.to(self.st_t["spawn_flags"].dtype))
         self._may_spawn = True
         self.planes_ok.zero_()
-        self.scratch[8 * self.B + 2:8 * self.B + 8].zero_()
+        self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()
         self._last_step = None
         self._synced = (int(self.st_t["episodes"].sum().item()),
                         int(self.st_t["episodes"].sum().item())
@@ -617,7 +546,6 @@ class SafeLifeVecEnv:
         """Restore a state_dict().  The start boards are restored from the dict and
         read from HBM (start_roll = -1), so level_index is informational: a snapshot
         taken before a swap to a smaller pool restores, with a warning."""
-        self._flush_resets()
         li = d["level_index"]
         if int(li.min().item()) < 0 or int(li.max().item()) >= self.pool.K:
             import warnings
