@@ -150,7 +150,15 @@ typedef struct sl_mt19937 {
     uint32_t *chains;
     uint32_t *prefix;
     uint32_t *polys;
-    int64_t *ctl;
+    int64_t *ctl;                   /* dev int64 [8] */
+    /* look-ahead (sl_mt19937_lookahead): after each fill, the blocks of the next
+     * fill's likely range are generated on this second stream, beside the step that
+     * consumes the current range; the next fill waits for them.  NULL = off.  The
+     * event handles and the flag are the library's. */
+    void *ahead_stream;
+    void *ev_fill, *ev_ahead;
+    int32_t ahead_pending;
+    int32_t reserved;
 } sl_mt19937;
 
 /* Seed: the stream of RandomState(seed), positioned so that draws from first_draw
@@ -159,9 +167,17 @@ typedef struct sl_mt19937 {
 int sl_mt19937_seed(sl_mt19937 *mt, uint32_t seed, int64_t first_draw, void *stream);
 /* Generate every not yet generated block holding a draw below *hi (dev int64);
  * *lo (dev) is the first draw the caller will read.  err (dev int64, may be NULL)
- * is OR-ed with 1 when the range cannot be served (re-seed). */
+ * is OR-ed with 1 when the range cannot be served (re-seed).  With the look-ahead
+ * on, `stream` first waits for the last fill's look-ahead, and after the fill the
+ * blocks of [*hi, *hi + 1.25 (*hi - *lo)) (capped by the ring) are generated on the
+ * look-ahead stream; mt's flag is updated (mt is const for the device state only). */
 int sl_mt19937_fill(const sl_mt19937 *mt, const int64_t *lo, const int64_t *hi, int64_t *err,
                     void *stream);
+/* Turn the look-ahead on (ahead_stream = a hipStream_t) or off (NULL); creates /
+ * keeps the two events.  sl_mt19937_release destroys them (the device buffers are
+ * the caller's). */
+int sl_mt19937_lookahead(sl_mt19937 *mt, void *ahead_stream);
+int sl_mt19937_release(sl_mt19937 *mt);
 /* Host reference pieces (no GPU): the seeded window, x^n mod phi, a jump of a
  * window by a polynomial, and n draws from a window (tests; seeding). */
 int sl_mt19937_host_window(uint32_t seed, uint32_t *window624);

@@ -69,7 +69,9 @@ class EnvCfg(ctypes.Structure):
 
 class MT19937(ctypes.Structure):
     _fields_ = [("n_chains", i32), ("rounds", i32), ("ring_draws", i64), ("ring", vp),
-                ("chains", vp), ("prefix", vp), ("polys", vp), ("ctl", vp)]
+                ("chains", vp), ("prefix", vp), ("polys", vp), ("ctl", vp),
+                ("ahead_stream", vp), ("ev_fill", vp), ("ev_ahead", vp),
+                ("ahead_pending", i32), ("reserved", i32)]
 
 
 class Capture(ctypes.Structure):
@@ -136,6 +138,8 @@ def lib():
             getattr(L, name).restype = ctypes.c_int
     mt = {"sl_mt19937_seed": [ctypes.POINTER(MT19937), u32, i64, vp],
           "sl_mt19937_fill": [ctypes.POINTER(MT19937), vp, vp, vp, vp],
+          "sl_mt19937_lookahead": [ctypes.POINTER(MT19937), vp],
+          "sl_mt19937_release": [ctypes.POINTER(MT19937)],
           "sl_mt19937_host_window": [u32, vp],
           "sl_mt19937_host_jump_poly": [u64, vp],
           "sl_mt19937_host_jump": [vp, vp, vp],

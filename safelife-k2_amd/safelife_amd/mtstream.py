@@ -30,10 +30,13 @@ class MT19937Stream:
 
     ``ring_draws``: doubles the ring holds (power of two); a step may read at most
     ``ring_draws`` minus one block.  ``n_chains``: blocks one fill can generate (power of
-    two); ``rounds``: a block is 624 * rounds raw outputs (312 * rounds draws)."""
+    two); ``rounds``: a block is 624 * rounds raw outputs (312 * rounds draws).
+    ``lookahead``: after each fill, generate the next fill's likely blocks (1.25x the
+    last range, past it) on a second stream beside the step that reads this fill's, the
+    next fill waiting for them (a single stream of consecutive ranges: one shard)."""
 
     def __init__(self, seed, device, *, first_draw=0, ring_draws=1 << 24, n_chains=None,
-                 rounds=420):
+                 rounds=420, lookahead=False):
         import torch
         self.torch = torch
         self.device = _lib.require_device(device)
@@ -50,13 +53,28 @@ class MT19937Stream:
         self.chains = torch.zeros(self.n_chains, MT_N, dtype=torch.int32, device=dev)
         self.prefix = torch.zeros(self.n_chains, PREFIX, dtype=torch.int32, device=dev)
         self.polys = torch.zeros(nk + 1, POLY_WORDS, dtype=torch.int32, device=dev)
-        self.ctl = torch.zeros(6, dtype=torch.int64, device=dev)
+        self.ctl = torch.zeros(8, dtype=torch.int64, device=dev)
         s = _lib.MT19937()
         s.n_chains, s.rounds, s.ring_draws = self.n_chains, self.rounds, self.ring_draws
         s.ring, s.chains, s.prefix = self.ring.data_ptr(), self.chains.data_ptr(), self.prefix.data_ptr()
         s.polys, s.ctl = self.polys.data_ptr(), self.ctl.data_ptr()
         self.struct = s
+        self._ahead = None
+        if lookahead:
+            # its kernels are latency-bound chains: a high-priority stream gets them
+            # dispatched among the step's waves
+            self._ahead = torch.cuda.Stream(device=dev, priority=-1)
+            _lib.check(_lib.lib().sl_mt19937_lookahead(ctypes.byref(s), self._ahead.cuda_stream),
+                       "sl_mt19937_lookahead")
         self.seek(first_draw)
+
+    def __del__(self):
+        try:
+            if self._ahead is not None:
+                self._ahead.synchronize()       # its kernels use this object's buffers
+            _lib.lib().sl_mt19937_release(ctypes.byref(self.struct))
+        except Exception:
+            pass
 
     @property
     def mask(self):
@@ -66,6 +84,8 @@ class MT19937Stream:
         """(Re-)seed so that draws from `first_draw` on can be generated (host
         polynomial work + device init; synchronises the device's current stream)."""
         L = _lib.lib()
+        if self._ahead is not None:
+            self._ahead.synchronize()           # a look-ahead still moving the chains
         _lib.check(L.sl_mt19937_seed(ctypes.byref(self.struct), self.seed, int(first_draw),
                                      _lib.stream_ptr(self.device)), "sl_mt19937_seed")
 

@@ -139,7 +139,8 @@ class SafeLifeVecEnv:
                 from .mtstream import MT19937Stream
                 self.mt = MT19937Stream(self.seed, self.device,
                                         ring_draws=max(1 << 22, self.n_total_envs * self.H *
-                                                       self.W // 4))
+                                                       self.W // 4),
+                                        lookahead=stream_exchange is None)
             else:
                 self.set_spawn_stream(spawn_stream)
         elif rng != "philox":
