@@ -33,13 +33,17 @@ def _ring_slice(torch, mt, lo, hi):
     return mt.ring[idx].cpu().numpy()
 
 
+@pytest.mark.parametrize("lookahead", [False, True])
 @pytest.mark.parametrize("rounds,n_chains,ring", [(33, 16, 1 << 21), (420, 64, 1 << 24)])
-def test_fill_matches_numpy(torch_dev, rounds, n_chains, ring):
+def test_fill_matches_numpy(torch_dev, rounds, n_chains, ring, lookahead):
     """Consecutive ranges, as replay steps consume the stream: empty, single draws,
-    block-sized and multi-block ranges, all equal to RandomState(s).random_sample."""
+    block-sized and multi-block ranges, all equal to RandomState(s).random_sample --
+    also with the look-ahead generating each next range's blocks on a second stream
+    while the test reads (and rewrites its range tensor for) the current one."""
     torch, dev = torch_dev
     from safelife_amd.mtstream import MT19937Stream
-    mt = MT19937Stream(2024, dev, ring_draws=ring, n_chains=n_chains, rounds=rounds)
+    mt = MT19937Stream(2024, dev, ring_draws=ring, n_chains=n_chains, rounds=rounds,
+                       lookahead=lookahead)
     D = mt.block
     ref = np.random.RandomState(2024).random_sample(6 * n_chains * D)
     rng = np.random.RandomState(0)
