@@ -63,7 +63,9 @@ class MT19937Stream:
         if lookahead:
             # its kernels are latency-bound chains: a high-priority stream gets them
             # dispatched among the step's waves
-            self._ahead = torch.cuda.Stream(device=dev, priority=-1)
+            import os
+            self._ahead = torch.cuda.Stream(
+                device=dev, priority=int(os.environ.get("SAFELIFE_MT_AHEAD_PRIORITY", "-1")))
             _lib.check(_lib.lib().sl_mt19937_lookahead(ctypes.byref(s), self._ahead.cuda_stream),
                        "sl_mt19937_lookahead")
         self.seek(first_draw)
