@@ -243,6 +243,43 @@ def test_mass_reset_on_one_step(torch_dev, obs):
     assert n_ep.min() >= 1 and n_ep.max() <= 2
 
 
+@pytest.mark.parametrize("pools", [(C3,), (C4, C3)])
+def test_full_batch_every_env_vs_c_oracle(torch_dev, pools):
+    """Every env of a full C3 batch (65 536; the C4 mix at 32 768), every step: rewards
+    and dones of the GPU batch against the C restatement of the chain
+    (oracle/sl_cpu_step.c, itself bit-exact with the oracle env, tests/test_cpu_step.py)
+    stepping the same batch on the host's cores, over 60 steps from reset with
+    time_limit 25 (two rounds of resets); then the boards and goals of every 16th env."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    levels = _levels(*pools)
+    B = 65536 if len(pools) == 1 else 32768
+    seed = 4321
+    kw = dict(time_limit=25, view_shape=(33, 33), penalty_coef=1.0, min_performance=0.01)
+    venv = SafeLifeVecEnv(LevelPool.load(*pools), B, dev, rng="philox", seed=seed,
+                          level_order="random", augment_roll=True, kernel="fast",
+                          compute_obs=False, output_channels=None, **kw)
+    venv.reset()
+    cb = oracle.CpuBatch(levels, B, seed=seed, level_order="random", augment_roll=True, **kw)
+    cb.reset()
+    threads = min(16, os.cpu_count() or 1)
+    rng = np.random.RandomState(12)
+    n_done = 0
+    for t in range(60):
+        acts = rng.randint(0, 9, size=B).astype(np.int32)
+        _, vr, vd, _ = venv.step(torch.from_numpy(acts).to(dev))
+        _, cr, cd = cb.step(acts, threads)
+        vr, vd = vr.cpu().numpy(), vd.cpu().numpy().astype(np.uint8)
+        bad = np.nonzero((vr != cr) | (vd != cd))[0]
+        assert bad.size == 0, (t, bad[:8], vr[bad[:4]], cr[bad[:4]])
+        n_done += int(cd.sum())
+    assert n_done >= B                      # every env crossed an episode end
+    vb, vg = venv.board.cpu().numpy(), venv.goals.cpu().numpy()
+    for e in range(0, B, 16):
+        assert np.array_equal(vb[e], cb.board(e, 0)), e
+        assert np.array_equal(vg[e], cb.board(e, 1)), e
+
+
 # ------------------------------------------------------------- (e) shard layouts
 @pytest.mark.parametrize("level_order,augment", [("random", True), ("sequential", False)])
 def test_two_shards_reproduce_one_run(torch_dev, level_order, augment):
