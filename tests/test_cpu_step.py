@@ -36,6 +36,7 @@ def _sprinkle(levels, rng, frac=0.01):
     ("c2_append_still_25", "sequential", False, True),
     ("c2_append_still_25", "random", True, True),
     ("c3_prune_still_64", "random", True, False),
+    ("c5_navigation_128", "random", True, False),
 ])
 def test_cpu_step_vs_oracle_env(pool, order, augment, obs):
     rng = np.random.RandomState(3)

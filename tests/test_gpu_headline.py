@@ -243,19 +243,24 @@ def test_mass_reset_on_one_step(torch_dev, obs):
     assert n_ep.min() >= 1 and n_ep.max() <= 2
 
 
-@pytest.mark.parametrize("pools", [(C3,), (C4, C3)])
+C5 = os.path.join(POOLS, "c5_navigation_128.npz")
+
+
+@pytest.mark.parametrize("pools", [(C3,), (C4, C3), (C5,)])
 def test_full_batch_every_env_vs_c_oracle(torch_dev, pools):
-    """Every env of a full C3 batch (65 536; the C4 mix at 32 768), every step: rewards
-    and dones of the GPU batch against the C restatement of the chain
-    (oracle/sl_cpu_step.c, itself bit-exact with the oracle env, tests/test_cpu_step.py)
-    stepping the same batch on the host's cores, over 60 steps from reset with
-    time_limit 25 (two rounds of resets); then the boards and goals of every 16th env."""
+    """Every env of a full C3 batch (65 536; the C4 mix at 32 768; C5's 128x128 levels
+    with spawners and per-step side effects at 4 096, the C restatement being slower
+    there), every step: rewards and dones of the GPU batch against the C restatement
+    of the chain (oracle/sl_cpu_step.c, itself bit-exact with the oracle env,
+    tests/test_cpu_step.py) stepping the same batch on the host's cores, from reset
+    over two rounds of resets; then the boards and goals of every 16th env."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
     levels = _levels(*pools)
-    B = 65536 if len(pools) == 1 else 32768
+    B = {1: 65536, 2: 32768}[len(pools)] if pools != (C5,) else 4096
+    T, tl = (60, 25) if pools != (C5,) else (30, 12)
     seed = 4321
-    kw = dict(time_limit=25, view_shape=(33, 33), penalty_coef=1.0, min_performance=0.01)
+    kw = dict(time_limit=tl, view_shape=(33, 33), penalty_coef=1.0, min_performance=0.01)
     venv = SafeLifeVecEnv(LevelPool.load(*pools), B, dev, rng="philox", seed=seed,
                           level_order="random", augment_roll=True, kernel="fast",
                           compute_obs=False, output_channels=None, **kw)
@@ -265,7 +270,7 @@ def test_full_batch_every_env_vs_c_oracle(torch_dev, pools):
     threads = min(16, os.cpu_count() or 1)
     rng = np.random.RandomState(12)
     n_done = 0
-    for t in range(60):
+    for t in range(T):
         acts = rng.randint(0, 9, size=B).astype(np.int32)
         _, vr, vd, _ = venv.step(torch.from_numpy(acts).to(dev))
         _, cr, cd = cb.step(acts, threads)
