@@ -113,6 +113,19 @@ int sl_advance(const uint16_t *in, uint16_t *out, int64_t B, int H, int W,
 int sl_count_eligible(const uint16_t *in, int64_t *counts, int64_t B, int H, int W,
                       void *stream);
 
+/*
+ * HOST advance of one board (no GPU; csrc/sl_host.cpp): speedups.advance_board's
+ * numpy path (module.c:19-44 for a numpy board).
+ *   in, out      host uint16 [H,W], row-major, must not alias; 2 <= H, 2 <= W <= 512.
+ *   draws        the caller's next n_draws spawn uniforms in reference order (one
+ *                per eligible cell, row-major, random.c:47-52).
+ * Returns the uniforms consumed (>= 0); -(needed + 1) when the board needs more
+ * than n_draws (out unspecified: call again with `needed`); with out == NULL, the
+ * number of eligible cells; INT64_MIN for a bad shape.  Thread-safe.
+ */
+int64_t sl_host_advance(const uint16_t *in, uint16_t *out, int64_t H, int64_t W,
+                        float spawn_prob, const double *draws, int64_t n_draws);
+
 /* out[i] = base + sum_{j<i} in[j]; *total_out (dev, may be NULL) = base + sum. */
 int sl_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n,
                           const int64_t *base, int64_t *total_out, void *stream);
@@ -134,13 +147,16 @@ int sl_exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n,
  *   chains   uint32 [n_chains, 624]          the MT state of each chain's next block
  *   prefix   uint32 [n_chains, SL_MT_PREFIX] scratch
  *   polys    uint32 [log2(n_chains) + 1, SL_MT_POLY_WORDS] jump polynomials
- *   ctl      int64 [6]: next block to generate, a done counter, error flags (bit0:
- *            a fill asked for a range the ring or the chains cannot serve), the
- *            first block, the next block whose chain has to jump, a done counter
+ *   ctl      int64 [SL_MT_CTL_WORDS] (8): [0] next block to generate, [1] a done
+ *            counter, [2] error flags (bit0: a fill asked for a range the ring or
+ *            the chains cannot serve), [3] the first block, [4] the next block whose
+ *            chain has to jump, [5] a done counter, [6] and [7] the last fill's draw
+ *            range [lo, hi) (written by every fill, read by the look-ahead)
  * n_chains is a power of two (one fill generates at most n_chains blocks), rounds
  * >= 33, ring_draws a power of two >= 2 blocks.
  */
 #define SL_MT_PREFIX 21216       /* 34 x 624 raw words */
+#define SL_MT_CTL_WORDS 8
 #define SL_MT_POLY_WORDS 640
 typedef struct sl_mt19937 {
     int32_t n_chains;
@@ -150,7 +166,7 @@ typedef struct sl_mt19937 {
     uint32_t *chains;
     uint32_t *prefix;
     uint32_t *polys;
-    int64_t *ctl;                   /* dev int64 [8] */
+    int64_t *ctl;                   /* dev int64 [SL_MT_CTL_WORDS] */
     /* look-ahead (sl_mt19937_lookahead): after each fill, the blocks of the next
      * fill's likely range are generated on this second stream, beside the step that
      * consumes the current range; the next fill waits for them.  NULL = off.  The

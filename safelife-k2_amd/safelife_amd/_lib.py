@@ -110,6 +110,9 @@ def lib():
                              u64, u32, u32, u32, vp, vp, vp]
     L.sl_count_eligible.argtypes = [vp, vp, i64, ctypes.c_int, ctypes.c_int, vp]
     L.sl_exclusive_scan_i64.argtypes = [vp, vp, i64, vp, vp, vp]
+    if hasattr(L, "sl_host_advance") or LIB_PATH == _DEFAULT_LIB:
+        L.sl_host_advance.argtypes = [vp, vp, i64, i64, f32, vp, i64]
+        L.sl_host_advance.restype = i64
     L.sl_copy16.argtypes = [vp, vp, i64, vp]
     L.sl_env_step.argtypes = [ctypes.POINTER(EnvState), ctypes.POINTER(LevelPool), vp,
                               ctypes.POINTER(EnvCfg), vp, vp, vp, vp, vp, vp]

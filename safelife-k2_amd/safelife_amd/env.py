@@ -84,7 +84,6 @@ class SafeLifeGame:
         self._pts = torch.zeros(1, dtype=torch.int32, device=venv.device)
         self._scratch = torch.zeros(8 + 16, dtype=torch.int64, device=venv.device)
         self._pos = torch.zeros(1, dtype=torch.int64, device=venv.device)
-        self._advances = 0           # Philox step counter of this game's own advances
 
     # ------------------------------------------------------------ construction
     @classmethod
@@ -392,8 +391,12 @@ class SafeLifeGame:
         elif v.rng != "stream":
             cfg.env0 = v.env0 + self._idx
             # (the top bit keeps these counters apart from the batch's step indices)
-            cfg.step = (0x80000000 | self._advances) & 0xFFFFFFFF
-            self._advances += 1
+            # the counter lives on the batch, per env, so that a SafeLifeGame made anew
+            # for the same env (every SafeLifeEnv.reset) does not repeat its draws
+            counts = v.__dict__.setdefault("_game_advances", {})
+            n = counts.get(self._idx, 0)
+            cfg.step = (0x80000000 | n) & 0xFFFFFFFF
+            counts[self._idx] = n + 1
         _lib.check(_lib.lib().sl_env_advance(ctypes.byref(self._slice()), ctypes.byref(cfg),
                                              self._stream()), "sl_env_advance")
         if ref:

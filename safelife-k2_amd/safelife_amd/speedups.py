@@ -3,20 +3,32 @@
     advance_board(board, spawn_prob=0.3) -> new uint16 board      module.c:19-44
     seed(i)                                                       module.c:246-253
 
-Both run on the GPU through libsafelife_hip.so.  Spawn draws follow the reference
-exactly: a 10 000-double buffer refilled from the *global* numpy RNG
-(``np.random.random(10000)``, random.c:14-26), one draw per eligible cell in
-row-major order (random.c:47-52), compared as ``u < (double)(float)spawn_prob``.
-The number of draws a board needs is counted on the GPU first, the host takes that
-many doubles from the emulated buffer, and the board is advanced on the GPU.
+Spawn draws follow the reference exactly: a 10 000-double buffer refilled from the
+*global* numpy RNG (``np.random.random(10000)``, random.c:14-26), one draw per
+eligible cell in row-major order (random.c:47-52), compared as
+``u < (double)(float)spawn_prob``.
+
+Where a board is advanced:
+  * numpy in -> numpy out: on the host, by the build's bit-sliced CPU engine
+    (``csrc/sl_host.cpp`` through the CPython module ``_native/_sl_host``), reading
+    its uniforms straight from the emulated buffer.  The reference's numpy callers
+    (side_effects.py:136-139, proc_gen.py:382,625) advance single small boards
+    thousands of times, where a device round trip would cost ~35x the reference's
+    own C call.  Boards wider than 512 cells go to the GPU path below;
+  * torch in -> torch out: on the GPU (libsafelife_hip.so): the draws a board needs
+    are counted on the device, the host takes that many doubles from the emulated
+    buffer, and the board is advanced on the device.
 
 Deliberate divergences: a non-2-d or empty board raises ValueError (the reference
 returns NULL without an exception, i.e. SystemError); H or W == 1 raises ValueError
-(undefined behaviour in the reference).
+(undefined behaviour in the reference).  ``seed`` truncates to 32 bits
+as the reference's ``"I"`` format does (module.c:248).
 
 ``advance_boards`` is the batched device entry (torch uint16 [B,H,W] in and out).
 """
 import ctypes
+import operator
+import sys
 
 import numpy as np
 
@@ -26,9 +38,21 @@ _RAND_BUFFER_SIZE = 10000
 
 
 class _RefBuffer:
+    """random.c's buffer: 10 000 doubles of np.random.random, refilled when used up.
+    The position lives in a one-element int64 array, which the host engine advances
+    in place."""
+
     def __init__(self):
-        self.buf = None
-        self.pos = _RAND_BUFFER_SIZE
+        self.buf = np.zeros(_RAND_BUFFER_SIZE)
+        self.posarr = np.full(1, _RAND_BUFFER_SIZE, np.int64)
+
+    @property
+    def pos(self):
+        return int(self.posarr[0])
+
+    @pos.setter
+    def pos(self, v):
+        self.posarr[0] = v
 
     def refill(self):
         self.buf = np.random.random(_RAND_BUFFER_SIZE)
@@ -45,7 +69,6 @@ class _RefBuffer:
             n -= k
         return np.concatenate(parts) if parts else np.zeros(0)
 
-
     def peek(self, n):
         """The next n draws without consuming them (numpy's global state and the
         buffer are restored)."""
@@ -61,12 +84,23 @@ _buffer = _RefBuffer()
 
 
 def seed(i):
-    """np.random.seed(i) followed by an immediate buffer refill (random.c:28-45)."""
-    i = int(i)
-    if not 0 <= i <= 0xFFFFFFFF:
-        raise OverflowError("seed must be an unsigned 32-bit int")
-    np.random.seed(i)
+    """np.random.seed(i) followed by an immediate buffer refill (random.c:28-45).
+
+    The reference parses ``i`` with PyArg_ParseTuple's "I" format (module.c:248):
+    any int, wrapped to 32 bits without an overflow check (a float is a TypeError)."""
+    np.random.seed(operator.index(i) & 0xFFFFFFFF)
     _buffer.refill()
+
+
+def _host():
+    global _HOST
+    if _HOST is None:
+        from ._native import _sl_host
+        _HOST = _sl_host
+    return _HOST
+
+
+_HOST = None
 
 
 def _to_device_board(board, device):
@@ -110,49 +144,91 @@ class _Frames:
         self.dn_np = self.dn_h.numpy()
 
 
+def _is_torch(x):
+    t = sys.modules.get("torch")
+    return t is not None and isinstance(x, t.Tensor)
+
+
 def advance_board(board, spawn_prob=0.3):
-    """Advance one board; returns a new array (numpy in -> numpy out, torch -> torch)."""
+    """Advance one board; returns a new array (numpy in -> numpy out on the host,
+    torch -> torch on the GPU)."""
+    b = _buffer
+    r = (_HOST or _host()).advance(board, spawn_prob, b.buf, b.posarr)
+    if r is not None and r is not NotImplemented:
+        return r                        # the common case: one C call
+    if _is_torch(board):
+        return _advance_device_torch(board, float(np.float32(spawn_prob)))
+    a = np.asarray(board)
+    if a.dtype != np.uint16 or not a.flags.c_contiguous or a.dtype.byteorder == ">":
+        a = np.ascontiguousarray(a, dtype=np.uint16)     # NPY_ARRAY_FORCECAST
+    if a.ndim != 2 or a.size == 0:
+        raise ValueError("advance_board expects a non-empty 2-d board")
+    H, W = a.shape
+    if H < 2 or W < 2:
+        raise ValueError("advance_board needs H, W >= 2")
+    if W > 512:
+        return _advance_device_numpy(a, float(np.float32(spawn_prob)))
+    if b.pos >= _RAND_BUFFER_SIZE:
+        b.refill()
+    r = _host().advance(a, spawn_prob, b.buf, b.posarr)
+    if r is not None:
+        return r
+    # the board needs more uniforms than the buffer still holds: take them as the
+    # reference does (refilled from the global stream when the buffer runs out)
+    return _host().advance_with(a, spawn_prob, b.take(_host().count_eligible(a)))
+
+
+def _advance_device_numpy(a, p):
+    """A numpy board too wide for the host engine: one copy up, count + advance on
+    the device, one copy down."""
     import torch
     device = _lib.require_device()
-    p = float(np.float32(spawn_prob))
     L = _lib.lib()
     s = _lib.stream_ptr(device)
-    if not isinstance(board, torch.Tensor):
-        a = np.asarray(board)
-        if a.ndim != 2 or a.size == 0:
-            raise ValueError("advance_board expects a non-empty 2-d board")
-        H, W = a.shape
-        if H < 2 or W < 2:
-            raise ValueError("advance_board needs H, W >= 2")
-        f = _Frames.get(H, W, device)
-        n = H * W
-        f.up_np[:2 * n] = np.ascontiguousarray(a, dtype=np.uint16).reshape(-1).view(np.uint8)
-        f.up_np[f.nb:] = _buffer.peek(n).view(np.uint8)
-        f.up_d.copy_(f.up_h, non_blocking=True)
-        bd = f.up_d.data_ptr()
-        _lib.check(L.sl_count_eligible(bd, f.dn_d.data_ptr() + f.nb, 1, H, W, s),
-                   "sl_count_eligible")
-        _lib.check(L.sl_advance(bd, f.dn_d.data_ptr(), 1, H, W, None, p, _lib.SL_RNG_STREAM,
-                                0, 0, 0, 0, bd + f.nb, f.off.data_ptr(), s), "sl_advance")
-        f.dn_h.copy_(f.dn_d, non_blocking=True)
-        torch.cuda.current_stream(device).synchronize()
-        _buffer.take(int(f.dn_np[f.nb:].view(np.int64)[0]))   # consumed whatever p is
-        return f.dn_np[:2 * n].view(np.uint16).reshape(H, W).copy()
+    H, W = a.shape
+    f = _Frames.get(H, W, device)
+    n = H * W
+    f.up_np[:2 * n] = np.ascontiguousarray(a, dtype=np.uint16).reshape(-1).view(np.uint8)
+    f.up_np[f.nb:] = _buffer.peek(n).view(np.uint8)
+    f.up_d.copy_(f.up_h, non_blocking=True)
+    bd = f.up_d.data_ptr()
+    _lib.check(L.sl_count_eligible(bd, f.dn_d.data_ptr() + f.nb, 1, H, W, s),
+               "sl_count_eligible")
+    _lib.check(L.sl_advance(bd, f.dn_d.data_ptr(), 1, H, W, None, p, _lib.SL_RNG_STREAM,
+                            0, 0, 0, 0, bd + f.nb, f.off.data_ptr(), s), "sl_advance")
+    f.dn_h.copy_(f.dn_d, non_blocking=True)
+    torch.cuda.current_stream(device).synchronize()
+    _buffer.take(int(f.dn_np[f.nb:].view(np.int64)[0]))   # consumed whatever p is
+    return f.dn_np[:2 * n].view(np.uint16).reshape(H, W).copy()
+
+
+def _advance_device_torch(board, p):
+    """A torch board on the device: the board's draws (at most one per cell) are
+    peeked from the emulated buffer and uploaded with it, count and advance run
+    back to back, and the one host sync reads the count the buffer then consumes."""
+    import torch
+    device = _lib.require_device()
+    L = _lib.lib()
+    s = _lib.stream_ptr(device)
     t, _ = _to_device_board(board, device)
     if t.dim() != 2 or t.numel() == 0:
         raise ValueError("advance_board expects a non-empty 2-d board")
     H, W = t.shape
     if H < 2 or W < 2:
         raise ValueError("advance_board needs H, W >= 2")
-    cnt = torch.zeros(1, dtype=torch.int64, device=device)
-    _lib.check(L.sl_count_eligible(t.data_ptr(), cnt.data_ptr(), 1, H, W, s), "sl_count_eligible")
-    n = int(cnt.item())
-    draws = _buffer.take(n)               # consumed whatever p is, as random_float() is
-    d = torch.from_numpy(draws if n else np.zeros(1)).to(device)
-    off = torch.zeros(1, dtype=torch.int64, device=device)
+    f = _Frames.get(H, W, device)
+    n = H * W
+    f.up_np[f.nb:] = _buffer.peek(n).view(np.uint8)
+    f.up_d.copy_(f.up_h, non_blocking=True)
     out = torch.empty_like(t)
+    cnt = f.dn_d.data_ptr() + f.nb
+    _lib.check(L.sl_count_eligible(t.data_ptr(), cnt, 1, H, W, s), "sl_count_eligible")
     _lib.check(L.sl_advance(t.data_ptr(), out.data_ptr(), 1, H, W, None, p, _lib.SL_RNG_STREAM,
-                            0, 0, 0, 0, d.data_ptr(), off.data_ptr(), s), "sl_advance")
+                            0, 0, 0, 0, f.up_d.data_ptr() + f.nb, f.off.data_ptr(), s),
+               "sl_advance")
+    f.dn_h[f.nb:].copy_(f.dn_d[f.nb:], non_blocking=True)
+    torch.cuda.current_stream(device).synchronize()
+    _buffer.take(int(f.dn_np[f.nb:].view(np.int64)[0]))   # consumed whatever p is
     return out
 
 

@@ -134,7 +134,9 @@ class SafeLifeVecEnv:
             if spawn_stream is None:
                 # the reference's seeded stream, generated on the device: the ring holds
                 # a quarter of a cell per env (C5's steady state draws 1/12), and one
-                # fill can generate a whole ring
+                # fill can generate a whole ring.  A step drawing more (at most 2 per
+                # cell: every board and goal cell eligible) sets the error flag, which
+                # step_async polls (_poll_stream_error) and stream_error() reads
                 self.spawn_stream = None
                 from .mtstream import MT19937Stream
                 self.mt = MT19937Stream(self.seed, self.device,
@@ -426,6 +428,29 @@ class SafeLifeVecEnv:
         launch()
         self._step_index += 1
         self.global_counter.num_steps += self.B
+        if self.mt is not None and self._step_index % self.STREAM_CHECK_EVERY == 0:
+            self._poll_stream_error()
+
+    # the device generator's error flag is polled every this many steps, without a sync
+    STREAM_CHECK_EVERY = 16
+
+    def _poll_stream_error(self):
+        """rng='stream' with the device generator: a step whose range the ring cannot
+        serve (a fill wider than the ring, or rewound below it) sets the error flag
+        and the replay would read stale draws.  The flag is copied to pinned host
+        memory behind the step (no sync) and the copy of the last poll is read, so a
+        failure raises at most 2 * STREAM_CHECK_EVERY steps late."""
+        torch = self.torch
+        if getattr(self, "_err_h", None) is None:
+            self._err_h = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            self._err_ev = None
+        if self._err_ev is not None and self._err_ev.query() and int(self._err_h[0]) & 1:
+            raise RuntimeError("rng='stream': the device generator could not serve a step's "
+                               "draw range (ring too small for the draws per step, or a "
+                               "rewind); re-seed with seek_stream / a larger ring")
+        self._err_h.copy_(self.scratch[8 * self.B:8 * self.B + 1], non_blocking=True)
+        self._err_ev = torch.cuda.Event()
+        self._err_ev.record(torch.cuda.current_stream(self.device))
 
     def _check_reset_lists(self):
         """Zero the per-parity reset-list lengths (scratch[8B+2 : 8B+4]) unless this

@@ -70,8 +70,12 @@ def test_no_gpu_fails_loudly():
         pytest.skip("GPU present")
     from safelife_amd import speedups, _lib
     import numpy as np
+    # numpy boards take the host engine; the device entries fail loudly
+    assert speedups.advance_board(np.zeros((4, 4), np.uint16)).shape == (4, 4)
     with pytest.raises(_lib.HipUnavailable):
-        speedups.advance_board(np.zeros((4, 4), np.uint16))
+        speedups.advance_board(torch.zeros((4, 4), dtype=torch.uint16))
+    with pytest.raises(_lib.HipUnavailable):
+        speedups.advance_boards(torch.zeros((2, 4, 4), dtype=torch.uint16))
     from safelife_amd import SafeLifeEnv, SafeLifeVecEnv, LevelPool
     from safelife_amd.side_effects import side_effect_densities
     level = {"board": np.zeros((8, 8), np.uint16), "goals": np.zeros((8, 8), np.uint16)}

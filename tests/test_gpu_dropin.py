@@ -272,6 +272,30 @@ def test_batch_view_advance_leaves_other_envs(torch_dev):
             assert torch.equal(v.goals[i], twin.goals[i]), (t, i)
 
 
+def test_view_advances_differ_across_game_objects(torch_dev):
+    """SafeLifeEnv.reset makes a new SafeLifeGame for the same env each episode; in
+    rng='philox' mode the advance counter lives on the batch, so a new game object's
+    advances do not repeat the draws of the last one's."""
+    import torch
+    from safelife_amd import SafeLifeGame, SafeLifeVecEnv, LevelPool
+    path = os.path.join(GOLDEN, "pools", "c5_navigation_128.npz")
+    v = SafeLifeVecEnv(LevelPool.load(path), 3, "cuda:0", rng="philox", seed=4,
+                       output_channels=None)
+    v.reset()
+    b0, g0 = v.board[1].clone(), v.goals[1].clone()
+    outs = []
+    for _ in range(2):
+        v.board[1].copy_(b0)
+        v.goals[1].copy_(g0)
+        v.planes_ok.zero_()
+        gv = SafeLifeGame(v, 1)
+        for _ in range(4):
+            gv.advance_board()
+        outs.append(v.board[1].clone())
+    assert int((b0 & 128 != 0).sum().item()) > 0          # the level has spawners
+    assert not torch.equal(outs[0], outs[1])
+
+
 def test_board_setter_on_128_replay_matches_generic(torch_dev):
     """Assigning game.board on a 128x128 replay env drops the draw planes the last
     step left (planes_ok bit 3), so the next replay steps count the new board's
