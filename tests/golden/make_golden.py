@@ -22,8 +22,12 @@ Fixtures and synthetic level pools (§8(d)):
   densities.npz               G5  _add_cell_distribution rollout densities
   levels/<name>.npz           benchmark levels used by the tests (data)
   pools/<name>.npz            proc-gen level pools for the benchmark configs
+  advance_known_answers_128.npz  G1 at 128x128, C5's board size (round 5)
+  advance_stream_128.npz         G2 at 128x128: C5 navigation levels, seeded stream
+  traj_nav128_*.npz              G4 at 128x128: PPO-chain trajectories on C5 levels
 
-Usage: python tests/golden/make_golden.py [--only g1,g2,traj,dens,pools,pool128]
+Usage: python tests/golden/make_golden.py [--only g1,g2,traj,dens,pools,pool128,
+                                                  g1_128,g2_128,traj128]
 """
 import argparse
 import hashlib
@@ -163,6 +167,65 @@ def gen_g1(out):
     print("G1", len(shapes), "boards ->", out)
 
 
+def gen_g1_128(out):
+    """G1 at C5's board size: random 128x128 boards (all used bits, life-like soups
+    with special cells, every bit pattern), one advance each at p in {0, 1} (no draw
+    decides anything).  Consecutive pairs share p, so a device test can step pair k
+    as one env's board and goals."""
+    from safelife import speedups
+    rng = np.random.RandomState(128)
+    used = np.uint16(0b1000111111111111)
+    ins, outs, probs = [], [], []
+    H = W = 128
+    for i in range(54):
+        dens = rng.uniform(0.05, 0.95)
+        mode = (i // 2) % 3
+        if mode == 0:
+            b = rng.randint(0, 1 << 16, size=(H, W)).astype(np.uint16) & used
+        elif mode == 1:
+            b = np.where(rng.rand(H, W) < 0.5, 9, 1).astype(np.uint16)
+            b |= (rng.randint(0, 8, size=(H, W)) << 9).astype(np.uint16)
+            special = rng.rand(H, W) < 0.1
+            b[special] |= rng.choice([16, 32, 64, 128, 152, 256, 4, 32768],
+                                     size=special.sum()).astype(np.uint16)
+        else:
+            b = rng.randint(0, 1 << 16, size=(H, W)).astype(np.uint16)
+        b = (b * (rng.rand(H, W) < dens)).astype(np.uint16)
+        p = float([0.0, 1.0][(i // 2) % 2])
+        speedups.seed(i)
+        ins.append(b)
+        outs.append(speedups.advance_board(b, p))
+        probs.append(p)
+    np.savez_compressed(out, boards_in=np.array(ins), boards_out=np.array(outs),
+                        spawn_prob=np.array(probs))
+    print("G1-128", len(ins), "boards ->", out)
+
+
+def gen_g2_128(out):
+    """G2 at 128x128: speedups.seed(s), then 30 advances of a C5 navigation level's
+    board and goals (board first), the level's own spawn_prob."""
+    from safelife import speedups
+    pool = np.load(os.path.join(HERE, "pools", "c5_navigation_128.npz"))
+    rec = {}
+    for s, k in ((21, 0), (22, 3)):
+        b0, g0 = pool["board"][k].copy(), pool["goals"][k].copy()
+        p = float(pool["spawn_prob"][k])
+        speedups.seed(s)
+        b, g = b0.copy(), g0.copy()
+        hb, hg = [], []
+        for t in range(30):
+            b = speedups.advance_board(b, p)
+            g = speedups.advance_board(g, p)
+            hb.append(b)
+            hg.append(g)
+        key = "s%d_l%d" % (s, k)
+        rec[key + "_board0"], rec[key + "_goals0"] = b0, g0
+        rec[key + "_boards"], rec[key + "_goals"] = np.array(hb), np.array(hg)
+        rec[key + "_p"] = np.float64(p)
+    np.savez_compressed(out, **rec)
+    print("G2-128 ->", out)
+
+
 def _spawner_boards(rng):
     from safelife.safelife_game import SafeLifeGame
     lv = np.load(os.path.join(REF, "safelife/levels/benchmarks/v1.0/append-spawn.npz"))["levels"]
@@ -233,6 +296,16 @@ TRAJ_SPECS = [
      dict(steps=800, penalty=1.0, min_perf=-1.0, seed=10, view=(33, 33), seek=0.85)),
     ("append_still_seek", ("archive", "benchmarks/v1.0/append-still.npz", 2),
      dict(steps=800, penalty=1.0, min_perf=0.0, seed=11, view=(15, 15), seek=0.85)),
+]
+# G4-128 (round 5): C5's board size -- 128x128 proc-gen navigation levels with
+# spawners and oscillators, the bench's wrapper settings, episodes short enough that
+# resets fall inside the trajectory
+TRAJ128_SPECS = [
+    ("nav128_c5", ("pool", "pools/c5_navigation_128.npz", 0),
+     dict(steps=400, penalty=1.0, min_perf=0.01, seed=12, view=(33, 33), time_limit=150)),
+    ("nav128_seek", ("pool", "pools/c5_navigation_128.npz", 3),
+     dict(steps=320, penalty=1.0, min_perf=0.01, seed=13, view=(33, 33), time_limit=120,
+          seek=0.8)),
 ]
 
 
@@ -443,7 +516,7 @@ def copy_levels():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="g1,g2,levels,pools,traj,dens")
+    ap.add_argument("--only", default="g1,g2,levels,pools,traj,dens,g1_128,g2_128,traj128")
     args = ap.parse_args()
     only = set(args.only.split(","))
     setup_reference()
@@ -463,6 +536,13 @@ def main():
             run_traj(name, src, **kw)
     if "dens" in only:
         gen_dens(os.path.join(HERE, "densities.npz"))
+    if "g1_128" in only:
+        gen_g1_128(os.path.join(HERE, "advance_known_answers_128.npz"))
+    if "g2_128" in only:
+        gen_g2_128(os.path.join(HERE, "advance_stream_128.npz"))
+    if "traj128" in only:
+        for name, src, kw in TRAJ128_SPECS:
+            run_traj(name, src, **kw)
 
 
 if __name__ == "__main__":

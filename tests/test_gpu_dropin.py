@@ -38,7 +38,7 @@ def _level(d):
 
 
 @pytest.mark.parametrize("name", ["append_still_v01", "append_spawn_v10", "prune_spawn_v10",
-                                  "append_still_seek", "prune_still_seek"])
+                                  "append_still_seek", "prune_still_seek", "nav128_c5"])
 def test_game_methods_replay_golden(torch_dev, name):
     """SafeLifeEnv.step's game calls one by one (execute_action -> advance_board ->
     current_points -> update_exit_colors; revert + update_exit_colors where the

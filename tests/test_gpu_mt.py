@@ -144,12 +144,27 @@ class _NumpyStream:
         return self.torch.from_numpy(self.a[sl])
 
 
-class _RingStream:
-    def __init__(self, torch, mt):
-        self.torch, self.mt = torch, mt
+class _HostJumpStream:
+    """RandomState(seed).random_sample at any position, from the host's own jump-ahead
+    (host_window / host_jump_poly / host_jump / host_draws, checked against numpy
+    itself in tests/test_mt_cpu.py): independent of the device ring.  Each request
+    jumps to its start and generates a chunk, so an env's board slice and the goals
+    slice after it cost one jump."""
+
+    def __init__(self, torch, seed, chunk=16384):
+        from safelife_amd.mtstream import host_window
+        self.torch, self.win, self.chunk = torch, host_window(seed), chunk
+        self.lo, self.a = 0, np.zeros(0)
+        self.jumps = 0
 
     def __getitem__(self, sl):
-        return self.torch.from_numpy(_ring_slice(self.torch, self.mt, sl.start, sl.stop))
+        from safelife_amd.mtstream import host_jump, host_jump_poly, host_draws
+        lo, hi = sl.start, sl.stop
+        if not (self.lo <= lo and hi <= self.lo + len(self.a)):
+            w = host_jump(self.win, host_jump_poly(2 * lo))
+            self.lo, self.a = lo, host_draws(w, max(hi - lo, self.chunk))
+            self.jumps += 1
+        return self.torch.from_numpy(self.a[lo - self.lo:hi - self.lo])
 
 
 def _seeded_steps(torch, dev, venv, oenvs, ostreams, sample, T, rng):
@@ -180,11 +195,12 @@ def test_seeded_replay_c5_full_batch_vs_numpy(torch_dev):
     """C5 at full batch with the stream generated on the device (what bench.py
     --rng seeded times; no rewind, no host buffer): for the first steps the sampled
     envs' oracles draw from numpy's own RandomState(SEED).random_sample at the device's
-    offsets; after 120 more steps (positions ~10^10) from the ring, whose slices are
-    then checked against the host jump at the sampled offsets."""
+    offsets; after 120 more steps (positions ~10^9) from the host's own jump-ahead to
+    each env's offsets -- never from the device ring -- for 31 steps, so every sampled
+    env's whole slice of every late step is the host's stream, and the ring's copy of
+    each slice equals it too."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
-    from safelife_amd.mtstream import host_window, host_jump, host_jump_poly, host_draws
     fname, B = CONFIGS["c5"]
     pool = LevelPool.load(os.path.join(POOLS, fname))
     venv = SafeLifeVecEnv(pool, B, dev, rng="stream", spawn_stream=None, seed=SEED,
@@ -216,14 +232,59 @@ def test_seeded_replay_c5_full_batch_vs_numpy(torch_dev):
         venv.step_async(torch.randint(0, 9, (B,), dtype=torch.int32, device=dev, generator=g))
     pos0 = int(venv.stream_pos.item())
     assert pos0 > 10 ** 9
-    sample, oenvs, ostreams = oracles(_RingStream(torch, venv.mt))
-    n_reset = _seeded_steps(torch, dev, venv, oenvs, ostreams, sample, 1, rng)
-    # the ring's slices of that step are numpy's stream (host jump from the seed)
-    offs = venv.scratch[2 * B:4 * B].cpu().numpy()
-    for e in sample[:4]:
-        lo = int(offs[2 * e])
-        ref = host_draws(host_jump(host_window(SEED), host_jump_poly(2 * lo)), 4000)
-        assert np.array_equal(_ring_slice(torch, venv.mt, lo, lo + 4000), ref), e
-    n_reset += _seeded_steps(torch, dev, venv, oenvs, ostreams, sample, 30, rng)
-    assert n_reset >= 6
+    host = _HostJumpStream(torch, SEED)
+    sample, oenvs, ostreams = oracles(host)
+    n_reset = 0
+    n_drawn = 0
+    for t in range(31):
+        n_reset += _seeded_steps(torch, dev, venv, oenvs, ostreams, sample, 1, rng)
+        # each sampled env's slice of this step (board then goals), as the ring holds it
+        offs = venv.scratch[2 * B:4 * B].cpu().numpy()
+        end = int(venv.stream_pos.item())
+        for e in sample:
+            lo = int(offs[2 * e])
+            hi = int(offs[2 * e + 2]) if 2 * e + 2 < 2 * B else end
+            if hi > lo:
+                assert np.array_equal(_ring_slice(torch, venv.mt, lo, hi),
+                                      host[lo:hi].numpy()), (t, e)
+                n_drawn += hi - lo
+    assert n_reset >= 6 and n_drawn > 10000 and host.jumps >= 31
     assert not venv.stream_error()
+
+
+def test_seeded_shards_equal_one_seeded_run(torch_dev):
+    """Parity mode over shards with the device generator: two shard envs, each with
+    its own MT19937 stream from the same seed and no look-ahead, placed by one
+    StreamExchange (each rank fills only its slice [base, base + total) of the
+    global stream: csrc/sl_mt.hip), reproduce one seeded 64-env C5 run bit for bit --
+    rewards, done flags, boards, goals and the stream position."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    from safelife_amd import dist as sdist
+    fname, _ = CONFIGS["c5"]
+    pool = LevelPool.load(os.path.join(POOLS, fname))
+    B = 64
+    kw = dict(KW, time_limit=25, level_order="random", augment_roll=True, seed=31,
+              spawn_stream=None, rng="stream", kernel="fast", compute_obs=False)
+    whole = SafeLifeVecEnv(pool, B, dev, **kw)
+    ex = sdist.StreamExchange(device=dev)
+    shards = [SafeLifeVecEnv(pool, B // 2, dev, env0=r * (B // 2), n_total_envs=B,
+                             stream_exchange=ex, **kw) for r in range(2)]
+    assert whole.mt is not None and all(s.mt is not None for s in shards)
+    whole.reset()
+    for s in shards:
+        s.reset()
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    for t in range(60):
+        a = torch.randint(0, 9, (B,), dtype=torch.int32, device=dev, generator=g)
+        _, r, d, _ = whole.step(a)
+        outs = [s.step(a[i * (B // 2):(i + 1) * (B // 2)]) for i, s in enumerate(shards)]
+        assert torch.equal(r, torch.cat([o[1] for o in outs])), t
+        assert torch.equal(d, torch.cat([o[2] for o in outs])), t
+        assert int(whole.stream_pos.item()) == int(ex.pos.item()), t
+        if t % 6 == 5:
+            assert torch.equal(whole.board, torch.cat([s.board for s in shards])), t
+            assert torch.equal(whole.goals, torch.cat([s.goals for s in shards])), t
+    assert int(ex.pos.item()) > 100000
+    assert not whole.stream_error() and not any(s.stream_error() for s in shards)

@@ -45,6 +45,32 @@ def test_g2_reference_stream():
             assert np.array_equal(g, d[key + "_goals"][t]), (key, t)
 
 
+def test_g1_128_known_answers():
+    """G1 at 128x128 (C5's board size), captured from the reference."""
+    d = np.load(os.path.join(GOLDEN, "advance_known_answers_128.npz"))
+    assert len(d["boards_in"]) >= 50
+    for b, want, p in zip(d["boards_in"], d["boards_out"], d["spawn_prob"]):
+        got, _ = oracle.advance(b, p, np.zeros(b.size), 0)
+        assert np.array_equal(got, want), p
+
+
+def test_g2_128_reference_stream():
+    """G2 at 128x128: C5 navigation levels advanced 30 times after speedups.seed(s)."""
+    d = np.load(os.path.join(GOLDEN, "advance_stream_128.npz"))
+    keys = sorted({k.rsplit("_", 1)[0] for k in d.files if k.endswith("_board0")})
+    assert len(keys) >= 2
+    for key in keys:
+        rng = oracle.RefStreamRNG()
+        rng.seed(int(key.split("_")[0][1:]))
+        p = float(d[key + "_p"])
+        b, g = d[key + "_board0"], d[key + "_goals0"]
+        for t in range(d[key + "_boards"].shape[0]):
+            b, _ = oracle.advance(b, p, rng.take(oracle.count_eligible(b)))
+            g, _ = oracle.advance(g, p, rng.take(oracle.count_eligible(g)))
+            assert np.array_equal(b, d[key + "_boards"][t]), (key, t)
+            assert np.array_equal(g, d[key + "_goals"][t]), (key, t)
+
+
 def _traj_files():
     return sorted(glob.glob(os.path.join(GOLDEN, "traj_*.npz")))
 

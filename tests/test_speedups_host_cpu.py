@@ -58,6 +58,25 @@ def test_g2_seeded_stream_through_numpy_path():
             assert np.array_equal(g, d[key + "_goals"][t]), (key, t)
 
 
+def test_g1_g2_128_through_numpy_path():
+    """The 128x128 fixtures (C5's board size, captured from the reference)."""
+    d = np.load(os.path.join(GOLDEN, "advance_known_answers_128.npz"))
+    for b, want, p in zip(d["boards_in"], d["boards_out"], d["spawn_prob"]):
+        speedups.seed(1)
+        assert np.array_equal(speedups.advance_board(b, p), want)
+    d = np.load(os.path.join(GOLDEN, "advance_stream_128.npz"))
+    keys = sorted({k.rsplit("_", 1)[0] for k in d.files if k.endswith("_board0")})
+    for key in keys:
+        speedups.seed(int(key.split("_")[0][1:]))
+        p = float(d[key + "_p"])
+        b, g = d[key + "_board0"], d[key + "_goals0"]
+        for t in range(d[key + "_boards"].shape[0]):
+            b = speedups.advance_board(b, p)
+            g = speedups.advance_board(g, p)
+            assert np.array_equal(b, d[key + "_boards"][t]), (key, t)
+            assert np.array_equal(g, d[key + "_goals"][t]), (key, t)
+
+
 def _spawner_soup(rng, H, W, dens=0.25):
     b = np.where(rng.rand(H, W) < dens, 9, 0).astype(np.uint16)
     b |= (rng.randint(0, 8, size=(H, W)) << 9).astype(np.uint16) * (b > 0)
