@@ -47,14 +47,20 @@ def _bare_env(torch, dev, boards, goals, spawn_prob, **kw):
     return env
 
 
-@pytest.mark.parametrize("kernel", ["fast", "generic"])
-def test_g1_128_known_answers(torch_dev, kernel):
+def test_g1_128_known_answers(torch_dev):
+    """Through the 128x128 step kernel (board and goals both advanced by the banded
+    rule), and through the batched per-cell advance (speedups.advance_boards).  (The
+    per-cell env step takes exits from the start board -- level exits are frozen and
+    recoloured every step -- so it is not a bare advance of all-bit boards.)"""
     torch, dev = torch_dev
+    from safelife_amd import speedups
     d = np.load(os.path.join(GOLDEN, "advance_known_answers_128.npz"))
     bi, bo, p = d["boards_in"], d["boards_out"], d["spawn_prob"]
     assert len(bi) >= 50 and np.array_equal(p[0::2], p[1::2])
-    env = _bare_env(torch, dev, bi[0::2], bi[1::2], p[0::2], rng="philox", seed=1,
-                    kernel=kernel)
+    out = speedups.advance_boards(torch.from_numpy(bi).to(dev),
+                                  torch.from_numpy(p.astype(np.float32)).to(dev)).cpu().numpy()
+    assert np.array_equal(out, bo)
+    env = _bare_env(torch, dev, bi[0::2], bi[1::2], p[0::2], rng="philox", seed=1)
     env.step(torch.zeros(env.B, dtype=torch.int32, device=dev))
     got_b, got_g = env.board.cpu().numpy(), env.goals.cpu().numpy()
     for k in range(env.B):
