@@ -19,7 +19,9 @@ the returns/advantages part of ``PPO.gen_training_batch`` (training/ppo.py:466-5
 
 Action uniforms come from Philox (``rng="philox"``; key = the env's seed, counter =
 (0, global env id, env-step index, 2)) or from a caller-supplied [T, N] float64
-array (``uniforms``), e.g. the reference's global numpy stream.
+array (``uniforms``), e.g. the reference's global numpy stream.  ``rng="reference"``
+replays the reference's loop itself -- envs one after another, actions and spawn
+refills from the one global numpy stream -- bit for bit (tests/golden g7_*.npz).
 """
 import ctypes
 from typing import Any, NamedTuple
@@ -93,18 +95,31 @@ def raise_choice_errors(err):
 
 
 def run_agents(venv, policy, steps_per_env, *, rnn_zero_state=None, uniforms=None,
-               check_probs=True):
+               check_probs=True, rng="batch"):
     """``PPO.run_agents`` for all ``venv.B`` envs at once (training/ppo.py:386-464).
 
     ``policy(obs, rnn_states) -> (probs [N, A], new_rnn_states)`` (ppo.py:436); obs
     is one [N, ...] slot of the states buffer.  ``uniforms``: optional float64
     [T, N] action draws (default: Philox keyed on venv.seed).  The env keeps its
     last observation and recurrent state between calls (env._ppo_last_obs /
-    _ppo_rnn_state, ppo.py:429-434)."""
+    _ppo_rnn_state, ppo.py:429-434).
+
+    ``rng="reference"`` (a SafeLifeVecEnv(rng="stream")): the reference's loop order
+    and its one global numpy stream, bit for bit after speedups.seed(s) -- per step
+    the probabilities come to the host once, and env after env draws its action with
+    np.random.choice (ppo.py:440) and then takes its step with its spawn draws from
+    speedups' buffer (SafeLifeVecEnv.step_env_reference, one host sync per env), so
+    the action draws and the buffer's refills interleave exactly as in the reference
+    (random.c:14-26).  A parity mode: one env at a time."""
     torch = _torch()
     T, N, dev = int(steps_per_env), venv.B, venv.device
     if T < 1:
         raise ValueError("steps_per_env must be >= 1")
+    if rng not in ("batch", "reference"):
+        raise ValueError("rng must be 'batch' or 'reference'")
+    if rng == "reference" and (uniforms is not None or venv.rng != "stream"):
+        raise ValueError("rng='reference' takes its draws from the global numpy stream and "
+                         "needs a SafeLifeVecEnv(rng='stream')")
     if uniforms is not None:
         uniforms = torch.as_tensor(uniforms, dtype=torch.float64).to(dev)
         if tuple(uniforms.shape) != (T, N):
@@ -127,6 +142,10 @@ def run_agents(venv, policy, steps_per_env, *, rnn_zero_state=None, uniforms=Non
     rnn = initial_rnn
     for t in range(T):
         probs, rnn = policy(states[t], rnn)
+        if rng == "reference":
+            _reference_step(venv, probs, t, actions, rewards, dones, states, flags, ep_len,
+                            ep_rew)
+            continue
         sample_actions(probs, seed=venv.seed, step=venv._step_index, env0=venv.env0,
                        uniforms=None if uniforms is None else uniforms[t], out=actions[t],
                        err=None if err is None else err[t], check=False)
@@ -146,6 +165,21 @@ def run_agents(venv, policy, steps_per_env, *, rnn_zero_state=None, uniforms=Non
     info = {"times_up": (flags & 1) != 0, "game_over": (flags & 2) != 0,
             "reset": (flags & 4) != 0, "episode_length": ep_len, "episode_reward": ep_rew}
     return Rollout(states, actions, rewards, dones.bool(), initial_rnn, info)
+
+
+def _reference_step(venv, probs, t, actions, rewards, dones, states, flags, ep_len, ep_rew):
+    """ppo.py:438-448 for slot t: env after env, np.random.choice on the host (numpy's
+    own checks and draw), then that env's step on the device."""
+    p = probs.detach()
+    p = p.cpu().numpy()
+    acts = np.empty(venv.B, np.int32)
+    for e in range(venv.B):
+        acts[e] = np.random.choice(len(p[e]), p=p[e])
+        venv.step_env_reference(e, int(acts[e]), reward_out=rewards[t], done_out=dones[t],
+                                obs_out=states[t + 1], flags_out=flags[t],
+                                ep_len_out=ep_len[t], ep_rew_out=ep_rew[t])
+    venv.end_reference_step()
+    actions[t].copy_(_torch().from_numpy(acts))
 
 
 def returns_advantages(rewards, end_episode, values, gamma=(0.99,), lmda=0.95,

@@ -116,6 +116,7 @@ class SafeLifeVecEnv:
         self._synced = (0, 0)        # (started, completed) already in global_counter
         self._recorder = None        # TrajectoryRecorder attached to this env
         self._draw_base = 0          # stream position of spawn_stream[0]
+        self._last_mode = None       # "batch" / "reference": how the last step ran
         self._alloc(obs_dtype)
         # may any env's board or goals hold a spawning cell (bit 7)?  Spawners come only
         # from levels (no rule or action creates one) unless powers can be toggled; when
@@ -400,6 +401,9 @@ class SafeLifeVecEnv:
         # keep a reference until the next step
         self._actions_in_flight = a
         L = _lib.lib()
+        if self._last_mode == "reference" and self.planes_ok is not None:
+            self.planes_ok.bitwise_and_(~8)     # (see step_env_reference)
+        self._last_mode = "batch"
         cfg = self._fill_cfg()
         self._check_reset_lists()
         cfg.capture = self._recorder._next_capture() if self._recorder is not None else None
@@ -451,6 +455,93 @@ class SafeLifeVecEnv:
         self._err_h.copy_(self.scratch[8 * self.B:8 * self.B + 1], non_blocking=True)
         self._err_ev = torch.cuda.Event()
         self._err_ev.record(torch.cuda.current_stream(self.device))
+
+    # ------------------------------------------------- the reference's PPO loop order
+    def step_env_reference(self, e, action, *, reward_out=None, done_out=None, obs_out=None,
+                           flags_out=None, ep_len_out=None, ep_rew_out=None):
+        """One env-step of env ``e`` alone, its spawn draws taken from the reference's
+        global numpy stream: speedups' emulated 10 000-double buffer, refilled from
+        np.random when it runs out (random.c:14-26,47-52).  The reference's PPO loop
+        steps its envs one after another (training/ppo.py:438-448), so env e's draws
+        follow the previous envs' draws and the np.random.choice calls in between in
+        one stream; rollout.run_agents(rng="reference") drives this.  The outputs
+        (full [B] tensors, like step_async's) get env e's entry.  The step runs the
+        replay kernels on the one-env slice (state_slice) with the next 2 H W draws
+        staged; one host sync reads how many it consumed, which the buffer then
+        gives up."""
+        from . import speedups
+        torch = self.torch
+        if self.rng != "stream":
+            raise ValueError("step_env_reference needs rng='stream'")
+        if self._recorder is not None:
+            raise ValueError("step_env_reference does not record (detach the recorder)")
+        if not 0 <= e < self.B:
+            raise IndexError("env %d outside [0, %d)" % (e, self.B))
+        fr = self._ref_frame()
+        if self._last_mode != "reference" and self.planes_ok is not None:
+            # the 128x128 replay keeps each env's next-step eligible count in the scratch
+            # (act[2B + b]); the reference steps keep theirs per env in fr["scratch"],
+            # so the draw planes are recounted from the board once on a switch
+            self.planes_ok.bitwise_and_(~8)
+        self._last_mode = "reference"
+        n2 = 2 * self.H * self.W
+        fr["draws_h"].numpy()[:] = speedups._buffer.peek(n2)
+        fr["draws_d"].copy_(fr["draws_h"], non_blocking=True)
+        fr["act_h"][0] = int(action)
+        fr["act_d"].copy_(fr["act_h"], non_blocking=True)
+        fr["pos"].zero_()
+        sc = fr["scratch"][e]
+        sc[8 + 2:8 + 4].zero_()
+        cfg = _lib.EnvCfg.from_buffer_copy(self._fill_cfg())
+        cfg.rng_mode = _lib.SL_RNG_STREAM
+        cfg.draws, cfg.n_draws = fr["draws_d"].data_ptr(), n2
+        cfg.stream_pos, cfg.mt = fr["pos"].data_ptr(), None
+        cfg.stream_phase, cfg.stream_base = 0, None
+        cfg.scratch = sc.data_ptr()
+        cfg.env0 = self.env0 + e
+        cfg.capture = None
+        obs = None
+        if self.compute_obs or obs_out is not None:
+            obs = (self.obs if obs_out is None else self._obs_target(obs_out))[e:e + 1]
+        self._fill_obs_cfg(cfg, obs)
+        outs = [self._out(o, d)[e:e + 1] for o, d in
+                ((reward_out, self.reward), (done_out, self.done), (flags_out, self.flags),
+                 (ep_len_out, self.ep_len), (ep_rew_out, self.ep_rew))]
+        st = self.state_slice(e, 1)
+        _lib.check(_lib.lib().sl_env_step(ctypes.byref(st), ctypes.byref(self._pool_dev["struct"]),
+                                          fr["act_d"].data_ptr(), ctypes.byref(cfg),
+                                          *[o.data_ptr() for o in outs],
+                                          _lib.stream_ptr(self.device)), "sl_env_step")
+        if self.stream_error_of(sc, 1):
+            raise RuntimeError("reference step consumed more draws than staged")
+        speedups._buffer.take(int(fr["pos"].item()))
+        self.global_counter.num_steps += 1
+
+    def end_reference_step(self):
+        """After every env took its step_env_reference: the batch's step index moves
+        on, and the batched reset lists start afresh."""
+        self._step_index += 1
+        self._last_step = None
+
+    def _ref_frame(self):
+        fr = getattr(self, "_ref_frame_data", None)
+        if fr is None:
+            torch, n2 = self.torch, 2 * self.H * self.W
+            fr = {"draws_h": torch.empty(n2, dtype=torch.float64, pin_memory=True),
+                  "draws_d": torch.empty(n2, dtype=torch.float64, device=self.device),
+                  "act_h": torch.empty(1, dtype=torch.int32, pin_memory=True),
+                  "act_d": torch.empty(1, dtype=torch.int32, device=self.device),
+                  "pos": torch.zeros(1, dtype=torch.int64, device=self.device),
+                  # one 1-env scratch per env: the 128x128 replay carries state in it
+                  # from one step of the env to the next
+                  "scratch": torch.zeros((self.B, 8 + 16), dtype=torch.int64,
+                                         device=self.device)}
+            self._ref_frame_data = fr
+        return fr
+
+    @staticmethod
+    def stream_error_of(scratch, B):
+        return bool(scratch[8 * B].item() & 1)
 
     def _check_reset_lists(self):
         """Zero the per-parity reset-list lengths (scratch[8B+2 : 8B+4]) unless this

@@ -25,9 +25,11 @@ Fixtures and synthetic level pools (§8(d)):
   advance_known_answers_128.npz  G1 at 128x128, C5's board size (round 5)
   advance_stream_128.npz         G2 at 128x128: C5 navigation levels, seeded stream
   traj_nav128_*.npz              G4 at 128x128: PPO-chain trajectories on C5 levels
+  g7_ppo_loop_*.npz              G7: the PPO rollout loop (ppo.py:436-452), 16 envs,
+                                 action draws and spawn refills in one global stream
 
 Usage: python tests/golden/make_golden.py [--only g1,g2,traj,dens,pools,pool128,
-                                                  g1_128,g2_128,traj128]
+                                                  g1_128,g2_128,traj128,g7]
 """
 import argparse
 import hashlib
@@ -421,6 +423,78 @@ def run_traj(name, src, steps, penalty, min_perf, seed, view, time_limit=1000, s
           "game_overs", int(out["game_over"].sum()), "->", os.path.basename(path))
 
 
+# G7 (round 5): the reference's PPO rollout loop itself (training/ppo.py:436-452) --
+# np.random.choice per env from the global numpy stream, env.step, env.reset on done --
+# over 16 envs, so the action draws and the spawn buffer's refills (random.c:14-26,
+# 47-52) interleave in one stream.  A fixed table policy stands in for the network.
+G7_SPECS = [
+    ("ppo_loop_spawn", ("archive", "benchmarks/v1.0/append-spawn.npz", 3),
+     dict(num_env=16, steps=40, seed=31, time_limit=15, penalty=1.0, min_perf=0.01)),
+    ("ppo_loop_nav128", ("pool", "pools/c5_navigation_128.npz", 1),
+     dict(num_env=16, steps=40, seed=32, time_limit=15, penalty=1.0, min_perf=0.01)),
+]
+
+
+def g7_table(num_env, steps, seed):
+    """The table policy: float32 action probabilities [steps, num_env, 9], as a
+    network's softmax would hand them to np.random.choice."""
+    t = np.random.RandomState(seed + 7000).dirichlet(np.ones(9) * 0.7, size=(steps, num_env))
+    t = t.astype(np.float32)
+    return t / t.sum(-1, keepdims=True)
+
+
+def run_ppo_loop(name, src, num_env, steps, seed, time_limit, penalty, min_perf):
+    from safelife import speedups
+    from safelife.safelife_env import SafeLifeEnv
+    from safelife.safelife_game import SafeLifeGame
+    from safelife import env_wrappers as ew
+    level_data = dict(load_level_data(src))
+
+    def level_iter():
+        while True:
+            yield SafeLifeGame.loaddata(level_data)
+
+    envs = []
+    for _ in range(num_env):
+        e0 = SafeLifeEnv(level_iter(), view_shape=(33, 33), time_limit=time_limit)
+        e = ew.MovementBonusWrapper(e0)
+        e = ew.SimpleSideEffectPenalty(e, penalty_coef=penalty, min_performance=min_perf)
+        envs.append((e0, ew.ContinuingEnv(e)))
+    table = g7_table(num_env, steps, seed)
+    speedups.seed(seed)
+    for e0, env in envs:                      # run_agents' first call (ppo.py:429-434)
+        env._ppo_last_obs = env.reset()
+    rec = {k: [] for k in ("action", "reward", "done", "board", "goals")}
+    for t in range(steps):                    # ppo.py:436-452
+        policies = table[t]
+        for (e0, env), policy in zip(envs, policies):
+            action = np.random.choice(len(policy), p=policy)
+            new_obs, reward, done, info = env.step(action)
+            if done:
+                new_obs = env.reset()
+            env._ppo_last_obs = new_obs
+            rec["action"].append(int(action))
+            rec["reward"].append(float(reward))
+            rec["done"].append(bool(done))
+            rec["board"].append(e0.game.board.copy())
+            rec["goals"].append(e0.game.goals.copy())
+    out = {k: np.array(v).reshape((steps, num_env) + np.array(v[0]).shape)
+           for k, v in rec.items()}
+    # boards and goals of every env at every 10th step (and the last) for 128x128
+    # levels (every step otherwise): rewards cover the steps in between
+    keep = np.arange(steps) if level_data["board"].size <= 4096 else \
+        np.unique(np.r_[np.arange(9, steps, 10), steps - 1])
+    out["board"], out["goals"], out["board_steps"] = out["board"][keep], out["goals"][keep], keep
+    out["table"] = table
+    out["after"] = np.random.random(4)        # where the global stream ended
+    for k in ("board", "goals", "agent_loc", "orientation", "spawn_prob", "min_performance"):
+        out["level_" + k] = np.asarray(level_data[k])
+    out["cfg"] = np.array([penalty, min_perf, seed, 33, 33, time_limit], np.float64)
+    path = os.path.join(HERE, "g7_%s.npz" % name)
+    np.savez_compressed(path, **out)
+    print("G7", name, "dones", int(out["done"].sum()), "->", os.path.basename(path))
+
+
 def gen_dens(out):
     """G5: the rollout + density half of side_effect_score (side_effects.py:131-143)."""
     from safelife import speedups
@@ -516,7 +590,7 @@ def copy_levels():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="g1,g2,levels,pools,traj,dens,g1_128,g2_128,traj128")
+    ap.add_argument("--only", default="g1,g2,levels,pools,traj,dens,g1_128,g2_128,traj128,g7")
     args = ap.parse_args()
     only = set(args.only.split(","))
     setup_reference()
@@ -543,6 +617,9 @@ def main():
     if "traj128" in only:
         for name, src, kw in TRAJ128_SPECS:
             run_traj(name, src, **kw)
+    if "g7" in only:
+        for name, src, kw in G7_SPECS:
+            run_ppo_loop(name, src, **kw)
 
 
 if __name__ == "__main__":

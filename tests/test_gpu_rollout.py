@@ -204,3 +204,60 @@ def test_obs_flat_tail_and_unaligned(torch_dev, dtype, ch):
         assert np.array_equal(un.float().cpu().numpy().astype(np.int64), c), t
         for k, bit in enumerate(ch):
             assert np.array_equal(c[..., k], (p >> bit) & 1), (t, k)
+
+
+@pytest.mark.parametrize("name", ["ppo_loop_spawn", "ppo_loop_nav128"])
+def test_run_agents_reference_order_g7(torch_dev, name):
+    """G7 (the reference's PPO loop, training/ppo.py:436-452, captured from the
+    reference: 16 envs, np.random.choice per env from the global stream that also
+    refills the spawn buffer) through run_agents(rng="reference") after
+    speedups.seed(s): actions, rewards, done flags, boards and goals bit-exact, and the
+    global numpy stream ends where the reference's did."""
+    torch, dev = torch_dev
+    from safelife_amd import SafeLifeVecEnv, LevelPool, speedups
+    from safelife_amd.rollout import run_agents
+    d = np.load(os.path.join(GOLDEN, "g7_%s.npz" % name))
+    penalty, min_perf, seed, vh, vw, time_limit = d["cfg"]
+    table = torch.from_numpy(d["table"]).to(dev)
+    T, N, A = table.shape
+    pool = LevelPool.from_levels([{
+        "board": d["level_board"], "goals": d["level_goals"], "agent_loc": d["level_agent_loc"],
+        "orientation": d["level_orientation"], "spawn_prob": d["level_spawn_prob"],
+        "min_performance": d["level_min_performance"]}])
+    venv = SafeLifeVecEnv(pool, N, dev, time_limit=int(time_limit), view_shape=(int(vh), int(vw)),
+                          output_channels=None, penalty_coef=float(penalty),
+                          min_performance=float(min_perf), rng="stream",
+                          spawn_stream=np.zeros(1))
+    step = [0]
+
+    def policy(obs, rnn):
+        p = table[step[0]]
+        step[0] += 1
+        return p, rnn
+
+    speedups.seed(int(seed))
+    boards, goals = [], []
+    keep = set(int(s) for s in d["board_steps"])
+    ro = None
+    for t in range(T):                 # one slot per call, boards read at the kept steps
+        ro = run_agents(venv, policy, 1, rng="reference")
+        assert np.array_equal(ro.actions[0].cpu().numpy(), d["action"][t]), t
+        assert np.array_equal(ro.rewards[0].cpu().numpy(), d["reward"][t]), t
+        assert np.array_equal(ro.end_episode[0].cpu().numpy(), d["done"][t]), t
+        if t in keep:
+            boards.append(venv.board.cpu().numpy())
+            goals.append(venv.goals.cpu().numpy())
+    assert np.array_equal(np.array(boards), d["board"])
+    assert np.array_equal(np.array(goals), d["goals"])
+    assert np.array_equal(np.random.random(4), d["after"])
+    # the whole loop in one call: the same rollout
+    venv2 = SafeLifeVecEnv(pool, N, dev, time_limit=int(time_limit),
+                           view_shape=(int(vh), int(vw)), output_channels=None,
+                           penalty_coef=float(penalty), min_performance=float(min_perf),
+                           rng="stream", spawn_stream=np.zeros(1))
+    step[0] = 0
+    speedups.seed(int(seed))
+    ro2 = run_agents(venv2, policy, T, rng="reference")
+    assert np.array_equal(ro2.actions.cpu().numpy(), d["action"])
+    assert np.array_equal(ro2.rewards.cpu().numpy(), d["reward"])
+    assert np.array_equal(venv2.board.cpu().numpy(), d["board"][-1])
