@@ -174,7 +174,16 @@ typedef struct sl_mt19937 {
     void *ahead_stream;
     void *ev_fill, *ev_ahead;
     int32_t ahead_pending;
-    int32_t reserved;
+    /* bit ring (round 5): bit_ring != 0 makes `ring` a ring of decisions -- draw d is
+     * bit (d & 31) of uint32 word (d & (ring_draws - 1)) >> 5 of ring (read as
+     * uint32_t, ring_draws / 8 bytes), set iff the draw's double is < bits_thr -- for
+     * batches whose envs all spawn with that one threshold (double)(float)p: the
+     * replay kernels need only u < p, and the ring then holds 1/64 of the bytes.
+     * rounds must be a multiple of 4 (a block's draws fill whole words).  A step whose
+     * env's threshold differs sets the stream error flag.  bit_ring == 0 (a zeroed
+     * struct): a ring of doubles, bits_thr unused. */
+    int32_t bit_ring;
+    double bits_thr;
 } sl_mt19937;
 
 /* Seed: the stream of RandomState(seed), positioned so that draws from first_draw

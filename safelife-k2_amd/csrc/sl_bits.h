@@ -174,6 +174,7 @@ struct StreamSrc {
     int64_t n;
     int64_t *err;
     int64_t mask = -1;      // StepArgs::draw_mask
+    const uint32_t *bits = nullptr;   // StepArgs::draw_bits
 };
 
 // Philox spawn draws of the eligible cells elig[w] (bit y of word w), per lane: the
@@ -355,7 +356,8 @@ __device__ __forceinline__ int stream_draws(const u32 elig[2], u32 sp[2], double
         for (int k = 0; k < 4; k++)
 #pragma unroll
             for (int w = 0; w < 2; w++)
-                u[k][w] = (e[k][w] && r[k][w] < src.n) ? src.draws[r[k][w] & src.mask] : 1.0;
+                u[k][w] = (e[k][w] && r[k][w] < src.n)
+                              ? stream_u(src.draws, src.bits, r[k][w], src.mask) : 1.0;
 #pragma unroll
         for (int k = 0; k < 4; k++)
 #pragma unroll

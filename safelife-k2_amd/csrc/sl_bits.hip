@@ -562,7 +562,7 @@ __device__ __forceinline__ void step_env(const sl_env_state &st, const StepArgs 
     sc.step = a.step;
     sc.seed = a.seed;
     set_spawn_prob(sc, __int_as_float(rec(V, R_SPAWN)));
-    StreamSrc ssrc{a.draws, a.n_draws, nullptr, a.draw_mask};
+    StreamSrc ssrc{a.draws, a.n_draws, nullptr, a.draw_mask, a.draw_bits};
     int64_t pos_b = 0, pos_g = 0;
     if (MODE == SPAWN_STREAM) {
         const Scratch w = scratch_of(fx.scratch, st.B);

@@ -333,7 +333,7 @@ k_env_step_bits128(Step128KArgs ka) {
     sc.step = a.step;
     sc.seed = a.seed;
     set_spawn_prob(sc, __int_as_float(rec(V, R_SPAWN)));
-    StreamSrc ssrc{a.draws, a.n_draws, nullptr, a.draw_mask};
+    StreamSrc ssrc{a.draws, a.n_draws, nullptr, a.draw_mask, a.draw_bits};
     int64_t pos_b = 0, pos_g = 0;
     if (MODE == SPAWN_STREAM) {
         ssrc.err = w.err;
@@ -853,6 +853,95 @@ k_stream_draw128(Step128KArgs ka) {
     draw_env128(ka, b, threadIdx.x, (int)w.act[ka.st.B + b], w.offsets[2 * b], w.offsets[2 * b + 1]);
 }
 
+// The draws from the device generator's bit ring (sl_mt.hip, sl_mt19937.bit_ring): the
+// ring holds the decisions (u < p) themselves, so a segment's spawns are its next
+// stream bits deposited into its eligible cells in order -- no slots, no uniforms,
+// no LDS (so more waves in flight), a 64-bit window of the ring per segment.  The
+// board's planes are loaded with the tensors-that-draw word and the offsets (one
+// round trip), the ring words after the ranks (a second).
+__global__ void __launch_bounds__(64)
+k_stream_draw128_bits(Step128KArgs ka) {
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const sl_env_state &st = ka.st;
+    const Scratch w = scratch_of(ka.fx.scratch, st.B);
+    u32 *dp = st.elig_planes + b * kEligStride + kDrawPlanes + lane;
+    const int dfl = (int)w.act[st.B + b];
+    const int64_t pos_t[2] = {w.offsets[2 * b], w.offsets[2 * b + 1]};
+    u32 E[NB][2];
+#pragma unroll
+    for (int t = 0; t < NB; t++)
+#pragma unroll
+        for (int q = 0; q < 2; q++) E[t][q] = dp[t * 128 + 64 * q];     // the board's
+    const double thr = (double)st.spawn_prob[b];
+    const uint32_t *bits = ka.a.draw_bits;
+    const int64_t draw_mask = ka.a.draw_mask, wmask = draw_mask >> 5;
+    const int half = lane >> 5;
+#pragma unroll 1
+    for (int tensor = 0; tensor < 2; tensor++) {
+        if (!((dfl >> tensor) & 1)) continue;
+        if (tensor == 1) {
+#pragma unroll
+            for (int t = 0; t < NB; t++)
+#pragma unroll
+                for (int q = 0; q < 2; q++) E[t][q] = dp[(NB + t) * 128 + 64 * q];
+        }
+        if (thr <= 0.0 || thr >= 1.0) {        // consumed, never compared (stream_draws)
+#pragma unroll
+            for (int t = 0; t < NB; t++)
+#pragma unroll
+                for (int q = 0; q < 2; q++)
+                    dp[(tensor * NB + t) * 128 + 64 * q] = thr >= 1.0 ? E[t][q] : 0u;
+            continue;
+        }
+        // segments (band, row, half) in stream order, as draw_env128 ranks them
+        int total = 0;
+        u32 R0[NB], R1[NB];
+        int64_t at[NB];
+#pragma unroll
+        for (int t = 0; t < NB; t++) {
+            R0[t] = transpose_halves(E[t][0], lane);
+            R1[t] = transpose_halves(E[t][1], lane);
+            const int c = __builtin_popcount(R0[t]) + __builtin_popcount(R1[t]);
+            const int cp = __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, c);
+            const int rc = c + cp;
+            const int incl = scan_halves(rc);
+            at[t] = (pos_t[tensor] + total + incl - rc + (half ? cp : 0)) & draw_mask;
+            total += __builtin_amdgcn_readlane(incl, 31);
+        }
+        u32 w0[NB], w1[NB], w2[NB];
+#pragma unroll
+        for (int t = 0; t < NB; t++) {          // every band's ring words in flight
+            const int64_t wi = at[t] >> 5;
+            w0[t] = bits[wi];
+            w1[t] = bits[(wi + 1) & wmask];
+            w2[t] = bits[(wi + 2) & wmask];
+        }
+#pragma unroll
+        for (int t = 0; t < NB; t++) {
+            const int sh = (int)(at[t] & 31);
+            uint64_t sb = ((((uint64_t)w1[t]) << 32) | w0[t]) >> sh;
+            if (sh) sb |= ((uint64_t)w2[t]) << (64 - sh);
+            u32 m = R0[t] | R1[t], s0 = 0u, s1 = 0u;
+            while (m) {
+                const int i = __builtin_ctz(m);
+                m &= m - 1u;
+                if ((R0[t] >> i) & 1u) {
+                    s0 |= (u32)(sb & 1u) << i;
+                    sb >>= 1;
+                }
+                if ((R1[t] >> i) & 1u) {
+                    s1 |= (u32)(sb & 1u) << i;
+                    sb >>= 1;
+                }
+            }
+            // back to the planes' layout (transpose_halves is an involution)
+            dp[(tensor * NB + t) * 128] = transpose_halves(s0, lane) & E[t][0];
+            dp[(tensor * NB + t) * 128 + 64] = transpose_halves(s1, lane) & E[t][1];
+        }
+    }
+}
+
 }  // namespace
 
 namespace sl {
@@ -877,7 +966,10 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
         const int rc = stream_offsets(st, fx, s);
         if (rc || !stream_steps(fx)) return rc;
         if (st.elig_planes) {       // draws decided up front
-            hipLaunchKernelGGL(k_stream_draw128, grid, dim3(64), 0, s, ka);
+            if (a.draw_bits)
+                hipLaunchKernelGGL(k_stream_draw128_bits, grid, dim3(64), 0, s, ka);
+            else
+                hipLaunchKernelGGL(k_stream_draw128, grid, dim3(64), 0, s, ka);
             if (hipGetLastError() != hipSuccess) return SL_EHIP;
             if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
             hipLaunchKernelGGL(k_env_step_bits128<SPAWN_DECIDED>, grid, dim3(64), 0, s, ka);

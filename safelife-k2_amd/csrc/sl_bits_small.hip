@@ -291,7 +291,7 @@ k_env_step_small(SmallKArgs ka) {
     int64_t pos_b = 0, pos_g = 0;
     if (MODE == SPAWN_STREAM) {
         const Scratch w = scratch_of(ka.scratch, st.B);
-        geo.src = StreamSrc{a.draws, a.n_draws, w.err, a.draw_mask};
+        geo.src = StreamSrc{a.draws, a.n_draws, w.err, a.draw_mask, a.draw_bits};
         pos_b = w.offsets[2 * b];
         pos_g = w.offsets[2 * b + 1];
     }
@@ -532,7 +532,8 @@ __device__ __forceinline__ void seg_stream(const u32 elig[2], u32 sp[2], double 
         for (int k = 0; k < 4; k++)
 #pragma unroll
             for (int w = 0; w < 2; w++)
-                u[k][w] = (draw && e[k][w] && r[k][w] < src.n) ? src.draws[r[k][w] & src.mask] : 1.0;
+                u[k][w] = (draw && e[k][w] && r[k][w] < src.n)
+                              ? stream_u(src.draws, src.bits, r[k][w], src.mask) : 1.0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             if (draw && ((e[k][0] && r[k][0] >= src.n) || (e[k][1] && r[k][1] >= src.n)))
@@ -721,7 +722,7 @@ k_env_step_seg4(SmallKArgs ka) {
     geo.src_r = (lane & ~15) + (active ? (j + 1 == nl ? 0 : j + 1) : j);
     geo.odd_last = (W & 1) && js == nl - 1;
     geo.real = active;
-    geo.src = StreamSrc{a.draws, a.n_draws, nullptr, a.draw_mask};
+    geo.src = StreamSrc{a.draws, a.n_draws, nullptr, a.draw_mask, a.draw_bits};
     geo.count = 0;
     const u32 wm0 = active ? geo.mh : 0u, wm1 = (active && !geo.odd_last) ? geo.mh : 0u;
     int64_t pos_b = 0, pos_g = 0;

@@ -14,6 +14,7 @@
 //   k_env_obs         get_obs + recenter_view (safelife_env.py:125-155,
 //                     helper_utils.py:41-74)
 #include "sl_env_common.h"
+#include "sl_env_action.h"
 #include "sl_obs.h"
 
 #include <math.h>
@@ -26,144 +27,14 @@ namespace {
 constexpr int NT = 256;
 constexpr int kMaxCells = 16384;          // board+goals in LDS: 64 KiB
 
-__device__ __forceinline__ void forward_vec(int orientation, int *fx, int *fy) {
-    // relative_loc(n_forward=1): dx=0, dy=-1 rotated clockwise `orientation` times
-    int dx = 0, dy = -1;
-    for (int k = 0; k < (orientation & 3); k++) {
-        int t = dx;
-        dx = -dy;
-        dy = t;
-    }
-    *fx = dx;
-    *fy = dy;
-}
-
-// ---------------------------------------------------------------------------
-// actions: one lane per env (cells touched: agent, front, behind, 2 ahead)
-// ---------------------------------------------------------------------------
-// (points, score, side-effect) terms of one cell; see cell_scores / side_term
-__device__ __forceinline__ void cell_terms(uint32_t bv, uint32_t gv, uint32_t sv, int *p, int *q,
-                                           int *se) {
-    int r;
-    cell_scores(bv, gv, p, q, &r);
-    *se = side_term(bv, sv, gv);
-}
-
-// The action edits at most the 4 cells agent / front / behind / two ahead.  DELTAS:
-// their contribution to the running scores is re-evaluated too (pre vs post edit, act
-// words 1-3), and the goals mirror is marked stale (the per-cell path does not keep
-// it); without DELTAS only the reward is written (the 128x128 kernel's pre-pass).
+// the action of every env, one lane each (sl_env_action.h)
 template <bool DELTAS>
 __global__ void __launch_bounds__(256)
 k_env_action(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int ctc,
              int64_t *__restrict__ act) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= st.B) return;
-    if (DELTAS && st.planes_ok) st.planes_ok[b] = 0;
-    const int H = st.H, W = st.W;
-    const int64_t hw = (int64_t)H * W;
-    uint16_t *bd = st.board + b * hw;
-    const uint16_t *gd = st.goals + b * hw, *sd = st.start_board + b * hw;
-    int reward = 0, d_pts = 0, d_scr = 0, d_side = 0;
-    uint32_t edit_rows = 0xFFFFFFFFu;      // rows the action may have edited (0xFF: none)
-    const int a = actions[b];
-    if (!st.game_over[b] && a >= 1 && a <= 8) {
-        const int orient = (a - 1) & 3;
-        st.orientation[b] = orient;
-        int fx, fy;
-        forward_vec(orient, &fx, &fy);
-        const int x0 = st.agent_x[b], y0 = st.agent_y[b];
-        const int x1 = pymod(x0 + fx, W), y1 = pymod(y0 + fy, H);
-        // distinct cells the action may touch
-        int cells[4] = {y0 * W + x0, y1 * W + x1, pymod(y0 - fy, H) * W + pymod(x0 - fx, W),
-                        pymod(y0 + 2 * fy, H) * W + pymod(x0 + 2 * fx, W)};
-        bool uniq[4];
-        for (int k = 0; k < 4; k++) {
-            uniq[k] = true;
-            for (int j = 0; j < k; j++) uniq[k] = uniq[k] && cells[j] != cells[k];
-        }
-        if (DELTAS)
-            for (int k = 0; k < 4; k++)
-                if (uniq[k]) {
-                    int p, q, se;
-                    cell_terms(bd[cells[k]], gd[cells[k]], sd[cells[k]], &p, &q, &se);
-                    d_pts -= p; d_scr -= q; d_side -= se;
-                }
-        if (a <= 4) {
-            // move_agent(1)
-            const int x2 = pymod(x0 - fx, W), y2 = pymod(y0 - fy, H);
-            int nx = x0, ny = y0;
-            uint32_t c1 = bd[y1 * W + x1];
-            if (c1 == 0) {
-                bd[y1 * W + x1] = bd[y0 * W + x0];
-                bd[y0 * W + x0] = 0;
-                nx = x1; ny = y1;
-            } else if ((c1 & EXIT) &&
-                       can_exit_now(st.min_performance[b], st.score[b], st.baseline[b],
-                                    st.possible[b])) {
-                st.game_over[b] = 1;
-                reward += 1;
-            } else if (c1 & PUSHABLE) {
-                const int x3 = pymod(x0 + 2 * fx, W), y3 = pymod(y0 + 2 * fy, H);
-                uint32_t c3 = bd[y3 * W + x3];
-                if (c3 == 0) {
-                    bd[y3 * W + x3] = bd[y1 * W + x1];
-                    bd[y1 * W + x1] = bd[y0 * W + x0];
-                    bd[y0 * W + x0] = 0;
-                    nx = x1; ny = y1;
-                } else if (c3 & EXIT) {
-                    bd[y1 * W + x1] = bd[y0 * W + x0];
-                    bd[y0 * W + x0] = 0;
-                    nx = x1; ny = y1;
-                }
-            }
-            const bool moved = (nx == x1 && ny == y1) && !(x0 == x1 && y0 == y1);
-            if (moved && (bd[y2 * W + x2] & PULLABLE)) {
-                bd[y0 * W + x0] = bd[y2 * W + x2];
-                bd[y2 * W + x2] = 0;
-            }
-            st.agent_x[b] = nx;
-            st.agent_y[b] = ny;
-        } else {
-            // TOGGLE
-            const uint32_t pc = bd[y0 * W + x0] & COLORS;
-            const uint32_t t = bd[y1 * W + x1];
-            if (t == 0) {
-                bd[y1 * W + x1] = (uint16_t)(LIFE | pc);
-            } else if (t & DESTR) {
-                bd[y1 * W + x1] = 0;
-            } else {
-                uint32_t tb = (ctp ? POWERS : 0u) | (ctc ? COLORS : 0u);
-                bd[y0 * W + x0] = (uint16_t)(bd[y0 * W + x0] ^ (t & tb));
-            }
-        }
-        if (DELTAS)
-            for (int k = 0; k < 4; k++)
-                if (uniq[k]) {
-                    int p, q, se;
-                    cell_terms(bd[cells[k]], gd[cells[k]], sd[cells[k]], &p, &q, &se);
-                    d_pts += p; d_scr += q; d_side += se;
-                }
-        // the 128x128 replay count mirror (sl_env_state.elig_planes) is behind by the
-        // rows of these cells: the count prologue re-reads them from the board
-        if (!DELTAS && st.elig_planes && H == 128 && W == 128) {
-            uint32_t rows = 0xFFFFFFFFu;
-            for (int k = 0; k < 4; k++) {
-                const uint32_t y = (uint32_t)(cells[k] >> 7);
-                bool seen = false;
-                for (int j = 0; j < 4; j++) seen = seen || ((rows >> (8 * j)) & 0xFFu) == y;
-                if (!seen) rows = (rows << 8) | y;
-            }
-            edit_rows = rows;
-        }
-    }
-    act[b] = reward;
-    if (!DELTAS && st.elig_planes) act[st.B + b] = (int64_t)edit_rows;
-    if (DELTAS) {
-        act[st.B + b] = d_pts;
-        act[2 * st.B + b] = d_scr;
-        act[3 * st.B + b] = d_side;
-    }
+    env_action_one<DELTAS>(st, actions, ctp, ctc, act, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -287,13 +158,13 @@ k_env_step_generic(sl_env_state st, StepArgs a, const int64_t *__restrict__ act,
             if (eb) {
                 if (thr <= 0.0) ub = 1.0;
                 else if (thr >= 1.0) ub = 0.0;
-                else if (pos_b + rb < a.n_draws) ub = a.draws[(pos_b + rb) & a.draw_mask];
+                else if (pos_b + rb < a.n_draws) ub = stream_u(a.draws, a.draw_bits, pos_b + rb, a.draw_mask);
                 else atomicOr((unsigned long long *)err, 1ull);
             }
             if (eg) {
                 if (thr <= 0.0) ug = 1.0;
                 else if (thr >= 1.0) ug = 0.0;
-                else if (pos_g + rg < a.n_draws) ug = a.draws[(pos_g + rg) & a.draw_mask];
+                else if (pos_g + rg < a.n_draws) ug = stream_u(a.draws, a.draw_bits, pos_g + rg, a.draw_mask);
                 else atomicOr((unsigned long long *)err, 1ull);
             }
             pos_b += tb;
@@ -370,13 +241,13 @@ k_env_advance(sl_env_state st, StepArgs a, const int64_t *__restrict__ offsets,
             if (eb) {
                 if (thr <= 0.0) ub = 1.0;
                 else if (thr >= 1.0) ub = 0.0;
-                else if (pos_b + rb < a.n_draws) ub = a.draws[(pos_b + rb) & a.draw_mask];
+                else if (pos_b + rb < a.n_draws) ub = stream_u(a.draws, a.draw_bits, pos_b + rb, a.draw_mask);
                 else atomicOr((unsigned long long *)err, 1ull);
             }
             if (eg) {
                 if (thr <= 0.0) ug = 1.0;
                 else if (thr >= 1.0) ug = 0.0;
-                else if (pos_g + rg < a.n_draws) ug = a.draws[(pos_g + rg) & a.draw_mask];
+                else if (pos_g + rg < a.n_draws) ug = stream_u(a.draws, a.draw_bits, pos_g + rg, a.draw_mask);
                 else atomicOr((unsigned long long *)err, 1ull);
             }
             pos_b += tb;
@@ -1015,8 +886,32 @@ extern "C" int sl_level_pool_prepare(sl_level_pool *pool, void *stream) {
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
+namespace {
+// A bit ring serves only envs whose threshold is the ring's: any env that draws this
+// step with another one flags the stream error (its spawns would be wrong).
+__global__ void __launch_bounds__(256)
+k_bits_thr_check(const float *__restrict__ spawn_prob, const int64_t *__restrict__ counts,
+                 int64_t B, double thr, int64_t *__restrict__ err) {
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b < B && (counts[2 * b] | counts[2 * b + 1]) && (double)spawn_prob[b] != thr)
+        atomicOr((unsigned long long *)err, 1ull);
+}
+}  // namespace
+
+int sl::bits_thr_check(const sl_env_state &st, const sl_mt19937 *mt, const int64_t *counts,
+                       int64_t *err, hipStream_t s) {
+    if (!mt || !mt->bit_ring || st.B == 0) return SL_OK;
+    hipLaunchKernelGGL(k_bits_thr_check, dim3((unsigned)((st.B + 255) / 256)), dim3(256), 0, s,
+                       st.spawn_prob, counts, st.B, mt->bits_thr, err);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
 int sl::stream_offsets(const sl_env_state &st, const FastExtra &fx, hipStream_t s) {
     const Scratch sc = scratch_of(fx.scratch, st.B);
+    if (fx.mt && fx.stream_phase != 2) {
+        const int rcb = bits_thr_check(st, fx.mt, sc.counts, sc.err, s);
+        if (rcb) return rcb;
+    }
     // phase 0: from the stream position; 1: from 0 (only the total matters, it lands
     // in *stream_pos); 2: from the shard's base the caller placed in *stream_base
     const int64_t *base = fx.stream_phase == 1 ? nullptr
@@ -1073,6 +968,10 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         a.draws = cfg->mt->ring;
         a.n_draws = INT64_MAX;
         a.draw_mask = cfg->mt->ring_draws - 1;
+        if (cfg->mt->bit_ring) {
+            a.draw_bits = reinterpret_cast<const uint32_t *>(cfg->mt->ring);
+            a.bits_thr = cfg->mt->bits_thr;
+        }
     }
     if (replay && (!cfg->stream_pos || (!a.draws && a.n_draws > 0))) return SL_EINVAL;
     if (cfg->stream_phase < 0 || cfg->stream_phase > 2 || (cfg->stream_phase && !replay) ||
@@ -1285,12 +1184,18 @@ extern "C" int sl_env_advance(sl_env_state *st, const sl_env_cfg *cfg, void *str
         a.draws = cfg->mt->ring;
         a.n_draws = INT64_MAX;
         a.draw_mask = cfg->mt->ring_draws - 1;
+        if (cfg->mt->bit_ring) {
+            a.draw_bits = reinterpret_cast<const uint32_t *>(cfg->mt->ring);
+            a.bits_thr = cfg->mt->bits_thr;
+        }
     }
     if (replay) {
         if (!set_lds((const void *)k_env_count, lds)) return SL_ETOOBIG;
         hipLaunchKernelGGL(k_env_count, dim3((unsigned)B), dim3(NT), lds, s, *st, sc.counts);
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
-        int rc = sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * B, cfg->stream_pos,
+        int rc = bits_thr_check(*st, cfg->mt, sc.counts, sc.err, s);
+        if (!rc)
+            rc = sl_exclusive_scan_i64(sc.counts, sc.offsets, 2 * B, cfg->stream_pos,
                                        cfg->stream_pos, stream);
         if (!rc && cfg->mt) rc = sl_mt19937_fill(cfg->mt, sc.offsets, cfg->stream_pos, sc.err, stream);
         if (rc) return rc;

@@ -47,7 +47,21 @@ struct StepArgs {
     int64_t n_draws;
     int64_t draw_mask = -1;      // draw r is draws[r & draw_mask]: -1 for a linear buffer,
                                  // ring_draws - 1 for the device generator's ring (sl_mt.hip)
+    const uint32_t *draw_bits = nullptr;   // the generator's bit ring (sl_mt19937.bit_ring):
+                                           // draw r below the ring's threshold iff bit r
+    double bits_thr = -1.0;                // that threshold
 };
+
+// Stream draw r as the replay kernels compare it (u < the env's threshold): the
+// supplied / generated double, or from a bit ring -1.0 (below) / 2.0 (not below) --
+// exact for an env whose threshold is the ring's (stream_offsets checks every drawing
+// env's, bits_thr_check)
+__device__ __forceinline__ double stream_u(const double *draws, const uint32_t *bits, int64_t r,
+                                           int64_t mask) {
+    const int64_t i = r & mask;
+    if (bits) return ((bits[i >> 5] >> (i & 31)) & 1u) ? -1.0 : 2.0;
+    return draws[i];
+}
 
 __device__ __forceinline__ int pymod(int a, int m) {
     int r = a % m;
@@ -340,6 +354,10 @@ __host__ inline bool stream_steps(const FastExtra &fx) { return fx.stream_phase 
 // replay mode: exclusive scan of the prologue's per-(env, tensor) eligible counts into
 // each tensor's first uniform, advancing *fx.stream_pos (sl_env.hip)
 int stream_offsets(const sl_env_state &st, const FastExtra &fx, hipStream_t s);
+// the device generator's bit ring: flag (err |= 1) any env with draws this step whose
+// threshold is not the ring's (sl_env.hip)
+int bits_thr_check(const sl_env_state &st, const sl_mt19937 *mt, const int64_t *counts,
+                   int64_t *err, hipStream_t s);
 // copies of the captured envs' state (sl_capture): phase 0 after the advance (and
 // the step's flags), phase 1 after the resets
 int launch_capture(const sl_env_state &st, const sl_capture &c, const uint8_t *flags, int phase,

@@ -71,7 +71,7 @@ class MT19937(ctypes.Structure):
     _fields_ = [("n_chains", i32), ("rounds", i32), ("ring_draws", i64), ("ring", vp),
                 ("chains", vp), ("prefix", vp), ("polys", vp), ("ctl", vp),
                 ("ahead_stream", vp), ("ev_fill", vp), ("ev_ahead", vp),
-                ("ahead_pending", i32), ("reserved", i32)]
+                ("ahead_pending", i32), ("bit_ring", i32), ("bits_thr", f64)]
 
 
 class Capture(ctypes.Structure):

@@ -195,6 +195,7 @@ class SafeLifeGame:
     @spawn_prob.setter
     def spawn_prob(self, v):
         self._set("spawn_prob", float(v))
+        self._venv._check_ring_threshold([float(v)])
 
     @property
     def min_performance(self):

@@ -26,7 +26,8 @@ def _pow2_at_least(n):
 
 
 class MT19937Stream:
-    """RandomState(seed).random_sample, draw d at ``ring[d & mask]`` on ``device``.
+    """RandomState(seed).random_sample, draw d at ``ring[d & mask]`` on ``device`` (or,
+    with ``bits_threshold``, the decision draw < threshold at bit d & mask of the ring).
 
     ``ring_draws``: doubles the ring holds (power of two); a step may read at most
     ``ring_draws`` minus one block.  ``n_chains``: blocks one fill can generate (power of
@@ -36,7 +37,7 @@ class MT19937Stream:
     next fill waiting for them (a single stream of consecutive ranges: one shard)."""
 
     def __init__(self, seed, device, *, first_draw=0, ring_draws=1 << 24, n_chains=None,
-                 rounds=420, lookahead=False):
+                 rounds=420, lookahead=False, bits_threshold=None):
         import torch
         self.torch = torch
         self.device = _lib.require_device(device)
@@ -49,7 +50,15 @@ class MT19937Stream:
         self.n_chains = _pow2_at_least(int(n_chains))
         nk = (self.n_chains - 1).bit_length()
         dev = self.device
-        self.ring = torch.empty(self.ring_draws, dtype=torch.float64, device=dev)
+        # bits_threshold: a ring of decisions (draw < threshold) for replay batches
+        # whose envs all spawn with that one threshold (double)(float)p: 1 bit per draw
+        self.bits_threshold = None if bits_threshold is None else float(bits_threshold)
+        if self.bits_threshold is not None:
+            if self.rounds % 4:
+                raise ValueError("a bit ring needs rounds % 4 == 0")
+            self.ring = torch.zeros(self.ring_draws // 32, dtype=torch.int32, device=dev)
+        else:
+            self.ring = torch.empty(self.ring_draws, dtype=torch.float64, device=dev)
         self.chains = torch.zeros(self.n_chains, MT_N, dtype=torch.int32, device=dev)
         self.prefix = torch.zeros(self.n_chains, PREFIX, dtype=torch.int32, device=dev)
         self.polys = torch.zeros(nk + 1, POLY_WORDS, dtype=torch.int32, device=dev)
@@ -58,6 +67,8 @@ class MT19937Stream:
         s.n_chains, s.rounds, s.ring_draws = self.n_chains, self.rounds, self.ring_draws
         s.ring, s.chains, s.prefix = self.ring.data_ptr(), self.chains.data_ptr(), self.prefix.data_ptr()
         s.polys, s.ctl = self.polys.data_ptr(), self.ctl.data_ptr()
+        if self.bits_threshold is not None:
+            s.bit_ring, s.bits_thr = 1, self.bits_threshold
         self.struct = s
         self._ahead = None
         if lookahead:
@@ -102,12 +113,21 @@ class MT19937Stream:
         return bool(self.ctl[2].item() & 1)
 
     def draws(self, lo, n):
-        """Draws [lo, lo + n) as a float64 device tensor (generating them first)."""
+        """Draws [lo, lo + n) as a float64 device tensor (generating them first); a bit
+        ring gives its decisions (draw < threshold) as a bool tensor."""
         torch = self.torch
         a = torch.tensor([int(lo), int(lo) + int(n)], dtype=torch.int64, device=self.device)
         self.fill(a[0:1], a[1:2])
-        idx = (torch.arange(int(lo), int(lo) + int(n), device=self.device) & self.mask)
-        return self.ring[idx]
+        return self.ring_slice(lo, lo + n)
+
+    def ring_slice(self, lo, hi):
+        """What the ring holds for draws [lo, hi) (no generation): float64 draws, or a
+        bit ring's decisions as bool."""
+        torch = self.torch
+        idx = (torch.arange(int(lo), int(hi), device=self.device) & self.mask)
+        if self.bits_threshold is None:
+            return self.ring[idx]
+        return ((self.ring[idx >> 5] >> (idx & 31).to(torch.int32)) & 1) != 0
 
 
 # ---------------------------------------------------------- host reference pieces

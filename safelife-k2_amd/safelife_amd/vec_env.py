@@ -73,7 +73,8 @@ class SafeLifeVecEnv:
                  auto_reset=True, rng="philox", seed=0, spawn_stream=None,
                  level_order="sequential", augment_roll=False, env0=0, n_total_envs=None,
                  can_toggle_powers=False, can_toggle_colors=False, obs_dtype="uint16",
-                 compute_obs=True, global_counter=None, kernel="auto", stream_exchange=None):
+                 compute_obs=True, global_counter=None, kernel="auto", stream_exchange=None,
+                 stream_ring="auto"):
         import torch
         self.torch = torch
         self.device = _lib.require_device(device)
@@ -107,6 +108,11 @@ class SafeLifeVecEnv:
         # rng="stream" over shards: dist.StreamExchange (or any callable of the same
         # contract) places this shard's draws in the global stream every step
         self.stream_exchange = stream_exchange
+        # the device generator's ring (rng='stream', spawn_stream=None): "auto" = a bit
+        # ring when every level spawns with one threshold, else doubles; "doubles"
+        if stream_ring not in ("auto", "doubles"):
+            raise ValueError("stream_ring must be 'auto' or 'doubles'")
+        self.stream_ring = stream_ring
         self._step_index = 0
         # step index and auto_reset flag of the last launched step: the 64x64 and
         # 128x128 kernels queue finished envs in per-parity lists (sl_env_cfg.scratch)
@@ -139,11 +145,8 @@ class SafeLifeVecEnv:
                 # cell: every board and goal cell eligible) sets the error flag, which
                 # step_async polls (_poll_stream_error) and stream_error() reads
                 self.spawn_stream = None
-                from .mtstream import MT19937Stream
-                self.mt = MT19937Stream(self.seed, self.device,
-                                        ring_draws=max(1 << 22, self.n_total_envs * self.H *
-                                                       self.W // 4),
-                                        lookahead=stream_exchange is None)
+                self.mt = self._make_mt(0, self._pool_threshold(self.pool)
+                                        if stream_ring == "auto" else None)
             else:
                 self.set_spawn_stream(spawn_stream)
         elif rng != "philox":
@@ -229,11 +232,61 @@ class SafeLifeVecEnv:
             raise ValueError("empty level pool")
         self.pool = pool
         self._pool_dev = pool_dev if pool_dev is not None else pool.to_device(self.device)
+        self._check_ring_threshold(pool.spawn_prob)
         # running envs keep their old-pool boards: the flag only grows here
         self._may_spawn = self._may_spawn or pool.has_spawners()
         # running episodes' start boards are no longer levels of the pool: the
         # kernels read them from HBM until those envs are reset from the new pool
         self.st_t["start_roll"].fill_(-1)
+
+    # ------------------------------------------------- the device generator's ring
+    @staticmethod
+    def _pool_threshold(pool):
+        """The one spawn threshold (double)(float)p of every level of the pool, or
+        None when they differ."""
+        t = set(float(np.float32(p)) for p in np.asarray(pool.spawn_prob).reshape(-1))
+        return t.pop() if len(t) == 1 else None
+
+    def _make_mt(self, first_draw, bits_threshold):
+        """The reference's seeded stream on the device (rng='stream', no spawn_stream):
+        a ring of a quarter of a cell per env (C5's steady state draws 1/12), one fill
+        able to generate a whole ring; a bit ring (decisions, not doubles) when every
+        env spawns with one threshold.  A step drawing more (at most 2 per cell) sets
+        the error flag, which step_async polls (_poll_stream_error)."""
+        from .mtstream import MT19937Stream
+        import os
+        # blocks: longer ones mean fewer chain jumps (one per block, the dominant cost
+        # once the ring holds bits and generation no longer writes HBM)
+        rounds = int(os.environ.get("SAFELIFE_MT_ROUNDS",
+                                    self.MT_ROUNDS_BITS if bits_threshold is not None else 420))
+        return MT19937Stream(self.seed, self.device, first_draw=first_draw,
+                             ring_draws=max(1 << 22, self.n_total_envs * self.H * self.W // 4),
+                             lookahead=self.stream_exchange is None,
+                             bits_threshold=bits_threshold, rounds=rounds)
+
+    MT_ROUNDS_BITS = 1680        # (C5 seeded, one box: 420 44.9 M, 840 47.5, 1680 48.6, 3360 27.3)
+
+    def _check_ring_threshold(self, probs=None):
+        """A bit ring serves only envs with its threshold: when spawn_prob may have
+        changed (set_state, load_state_dict, set_pool, a game's setter) and some env or
+        pool level no longer has it, the generator is rebuilt as a ring of doubles at
+        the current stream position."""
+        mt = self.mt
+        if mt is None or mt.bits_threshold is None:
+            return
+        if probs is None:
+            cur = self.st_t["spawn_prob"].to(self.torch.float64)
+            same = bool((cur == mt.bits_threshold).all().item())
+            same = same and self._pool_threshold(self.pool) == mt.bits_threshold
+        else:
+            same = all(float(np.float32(p)) == mt.bits_threshold
+                       for p in np.asarray(probs).reshape(-1))
+        if not same:
+            self.mt = None
+            self.torch.cuda.synchronize(self.device)
+            pos = getattr(self.stream_exchange, "pos", None)
+            self.mt = self._make_mt(int((pos if pos is not None else self.stream_pos).item()),
+                                    None)
 
     def set_spawn_stream(self, stream, pos=0):
         """Uniform doubles consumed in reference order (rng='stream'): a numpy array,
@@ -644,6 +697,7 @@ class SafeLifeVecEnv:
         self.planes_ok.zero_()
         self.scratch[8 * self.B + 2:8 * self.B + 4].zero_()
         self._last_step = None
+        self._check_ring_threshold()
         self._synced = (int(self.st_t["episodes"].sum().item()),
                         int(self.st_t["episodes"].sum().item())
                         - int(self._running_mask().sum().item()) - self._abandoned)

@@ -29,23 +29,29 @@ pytestmark = pytest.mark.gpu
 
 
 def _ring_slice(torch, mt, lo, hi):
-    idx = torch.arange(int(lo), int(hi), device=mt.device) & mt.mask
-    return mt.ring[idx].cpu().numpy()
+    return mt.ring_slice(lo, hi).cpu().numpy()
 
 
 @pytest.mark.parametrize("lookahead", [False, True])
-@pytest.mark.parametrize("rounds,n_chains,ring", [(33, 16, 1 << 21), (420, 64, 1 << 24)])
-def test_fill_matches_numpy(torch_dev, rounds, n_chains, ring, lookahead):
+@pytest.mark.parametrize("rounds,n_chains,ring,bits", [(33, 16, 1 << 21, None),
+                                                       (420, 64, 1 << 24, None),
+                                                       (36, 16, 1 << 21, 0.3),
+                                                       (1684, 8, 1 << 24, 0.3),
+                                                       (420, 64, 1 << 24, 0.30000001192092896)])
+def test_fill_matches_numpy(torch_dev, rounds, n_chains, ring, bits, lookahead):
     """Consecutive ranges, as replay steps consume the stream: empty, single draws,
     block-sized and multi-block ranges, all equal to RandomState(s).random_sample --
     also with the look-ahead generating each next range's blocks on a second stream
-    while the test reads (and rewrites its range tensor for) the current one."""
+    while the test reads (and rewrites its range tensor for) the current one.  A bit
+    ring holds draw < threshold for every draw."""
     torch, dev = torch_dev
     from safelife_amd.mtstream import MT19937Stream
     mt = MT19937Stream(2024, dev, ring_draws=ring, n_chains=n_chains, rounds=rounds,
-                       lookahead=lookahead)
+                       lookahead=lookahead, bits_threshold=bits)
     D = mt.block
     ref = np.random.RandomState(2024).random_sample(6 * n_chains * D)
+    if bits is not None:
+        ref = ref < bits
     rng = np.random.RandomState(0)
     lohi = torch.zeros(2, dtype=torch.int64, device=dev)
     pos, n_fills = 0, 0
@@ -108,16 +114,21 @@ def test_g2_reproduced_from_seed_alone(torch_dev):
     assert n_draws > 0
 
 
+@pytest.mark.parametrize("ring,kernel", [("auto", "fast"), ("doubles", "fast"),
+                                         ("auto", "generic")])
 @pytest.mark.parametrize("path", _traj_files(), ids=lambda p: os.path.basename(p)[5:-4])
-def test_golden_trajectory_from_seed_alone(torch_dev, path):
+def test_golden_trajectory_from_seed_alone(torch_dev, path, ring, kernel):
     """The reference-captured PPO-chain trajectories (speedups.seed(cfg seed), then
-    1 100 env steps) through the bit-sliced kernels with the spawn stream generated on
-    the device inside each step: boards, goals, rewards, views bit-exact."""
+    1 100 env steps) through the bit-sliced (and the per-cell) kernels with the spawn
+    stream generated on the device inside each step: boards, goals, rewards, views
+    bit-exact.  One level, one spawn probability: a bit ring ("auto"), and a ring of
+    doubles."""
     torch, dev = torch_dev
     d = np.load(path)
     seed = int(d["cfg"][2])
-    env = _vec_env_from_traj(d, kernel="fast", spawn_stream=None, seed=seed)
+    env = _vec_env_from_traj(d, kernel=kernel, spawn_stream=None, seed=seed, stream_ring=ring)
     assert env.mt is not None
+    assert (env.mt.bits_threshold is not None) == (ring == "auto")
     obs = env.reset().cpu().numpy()
     assert np.array_equal(obs[0], d["obs0"])
     actions = torch.from_numpy(d["action"].astype(np.int32)).to(dev)
@@ -245,24 +256,31 @@ def test_seeded_replay_c5_full_batch_vs_numpy(torch_dev):
             lo = int(offs[2 * e])
             hi = int(offs[2 * e + 2]) if 2 * e + 2 < 2 * B else end
             if hi > lo:
-                assert np.array_equal(_ring_slice(torch, venv.mt, lo, hi),
-                                      host[lo:hi].numpy()), (t, e)
+                want = host[lo:hi].numpy()
+                if venv.mt.bits_threshold is not None:      # C5's one p: a bit ring
+                    want = want < venv.mt.bits_threshold
+                assert np.array_equal(_ring_slice(torch, venv.mt, lo, hi), want), (t, e)
                 n_drawn += hi - lo
     assert n_reset >= 6 and n_drawn > 10000 and host.jumps >= 31
+    assert venv.mt.bits_threshold == float(np.float32(0.3))
     assert not venv.stream_error()
 
 
-def test_seeded_shards_equal_one_seeded_run(torch_dev):
+@pytest.mark.parametrize("ring", ["bits", "doubles"])
+def test_seeded_shards_equal_one_seeded_run(torch_dev, ring):
     """Parity mode over shards with the device generator: two shard envs, each with
     its own MT19937 stream from the same seed and no look-ahead, placed by one
     StreamExchange (each rank fills only its slice [base, base + total) of the
     global stream: csrc/sl_mt.hip), reproduce one seeded 64-env C5 run bit for bit --
-    rewards, done flags, boards, goals and the stream position."""
+    rewards, done flags, boards, goals and the stream position.  C5's levels share one
+    spawn probability (a bit ring); with one level's changed, rings of doubles."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
     from safelife_amd import dist as sdist
     fname, _ = CONFIGS["c5"]
     pool = LevelPool.load(os.path.join(POOLS, fname))
+    if ring == "doubles":
+        pool.spawn_prob[1] = 0.25
     B = 64
     kw = dict(KW, time_limit=25, level_order="random", augment_roll=True, seed=31,
               spawn_stream=None, rng="stream", kernel="fast", compute_obs=False)
@@ -271,6 +289,7 @@ def test_seeded_shards_equal_one_seeded_run(torch_dev):
     shards = [SafeLifeVecEnv(pool, B // 2, dev, env0=r * (B // 2), n_total_envs=B,
                              stream_exchange=ex, **kw) for r in range(2)]
     assert whole.mt is not None and all(s.mt is not None for s in shards)
+    assert (whole.mt.bits_threshold is not None) == (ring == "bits")
     whole.reset()
     for s in shards:
         s.reset()
