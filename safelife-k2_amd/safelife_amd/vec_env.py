@@ -264,7 +264,8 @@ class SafeLifeVecEnv:
                              lookahead=self.stream_exchange is None,
                              bits_threshold=bits_threshold, rounds=rounds)
 
-    MT_ROUNDS_BITS = 1680        # (C5 seeded, one box: 420 44.9 M, 840 47.5, 1680 48.6, 3360 27.3)
+    MT_ROUNDS_BITS = 840         # (C5 seeded, 128-thread generator blocks: 840 48.4 M,
+                                 # 1680 32.2; 256 threads: 420 44.9, 840 47.5-47.8, 1680 47.2-48.6)
 
     def _check_ring_threshold(self, probs=None):
         """A bit ring serves only envs with its threshold: when spawn_prob may have
