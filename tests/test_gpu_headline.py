@@ -246,19 +246,19 @@ def test_mass_reset_on_one_step(torch_dev, obs):
 C5 = os.path.join(POOLS, "c5_navigation_128.npz")
 
 
-@pytest.mark.parametrize("pools", [(C3,), (C4, C3), (C5,)])
-def test_full_batch_every_env_vs_c_oracle(torch_dev, pools):
+@pytest.mark.parametrize("pools,B,T,tl", [((C3,), 65536, 60, 25), ((C4, C3), 32768, 60, 25),
+                                          ((C5,), 4096, 30, 12), ((C5,), 65536, 16, 6)])
+def test_full_batch_every_env_vs_c_oracle(torch_dev, pools, B, T, tl):
     """Every env of a full C3 batch (65 536; the C4 mix at 32 768; C5's 128x128 levels
-    with spawners and per-step side effects at 4 096, the C restatement being slower
-    there), every step: rewards and dones of the GPU batch against the C restatement
-    of the chain (oracle/sl_cpu_step.c, itself bit-exact with the oracle env,
+    with spawners and per-step side effects at 4 096 over 30 steps, and at the full
+    65 536 over 16 steps of 6-step episodes, the C restatement being slower there),
+    every step: rewards and dones of the GPU batch against the C restatement of the
+    chain (oracle/sl_cpu_step.c, itself bit-exact with the oracle env,
     tests/test_cpu_step.py) stepping the same batch on the host's cores, from reset
     over two rounds of resets; then the boards and goals of every 16th env."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
     levels = _levels(*pools)
-    B = {1: 65536, 2: 32768}[len(pools)] if pools != (C5,) else 4096
-    T, tl = (60, 25) if pools != (C5,) else (30, 12)
     seed = 4321
     kw = dict(time_limit=tl, view_shape=(33, 33), penalty_coef=1.0, min_performance=0.01)
     venv = SafeLifeVecEnv(LevelPool.load(*pools), B, dev, rng="philox", seed=seed,
