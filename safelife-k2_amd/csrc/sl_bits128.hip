@@ -573,6 +573,16 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
     const u32 *gg = reinterpret_cast<const u32 *>(st.goals + off) + lane;
     const u32 V = load_record(st, ka.actions, b, lane);
     const Scratch w = scratch_of(ka.fx.scratch, st.B);
+    // the last step's band counts and the action's edited rows, loaded with the record
+    // rather than after it (count_next's first round trip), and waited for while the
+    // record is still in flight
+    uint64_t nc_pre = 0;
+    u32 rows_pre = 0xFFFFFFFFu;
+    if (st.elig_planes) {
+        nc_pre = (uint64_t)w.act[2 * st.B + b];
+        rows_pre = (u32)w.act[st.B + b];
+        asm volatile("" ::"s"(nc_pre), "s"(rows_pre));
+    }
     SpawnCtx sc{0u, 0u, 0ull, 0.0};
     const StreamSrc none{nullptr, 0, nullptr};
     // the draw planes: each counted tensor's eligible cells, for k_stream_draw128
@@ -610,10 +620,10 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
     // fit one window (the full count then runs).
     auto count_next = [&]() -> int {
         // their count, as the step left it (scratch act[2B + b]: four 16-bit band counts)
-        const uint64_t nc = (uint64_t)w.act[2 * st.B + b];
+        const uint64_t nc = nc_pre;
         const int n0 = (int)((nc & 0xFFFFu) + ((nc >> 16) & 0xFFFFu) + ((nc >> 32) & 0xFFFFu) +
                              (nc >> 48));
-        const u32 rows = (u32)w.act[st.B + b];
+        const u32 rows = rows_pre;
         int y0 = -1, dmin = 0, dmax = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -627,6 +637,16 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
         if (y0 < 0) return n0;                          // nothing edited: as the step left it
         if (dmax - dmin > 27) return -1;
         const int base = (y0 + dmin - 2) & (N - 1), nrows = dmax - dmin + 5;
+        // the window spans band tb from bit sh on and, when sh > 0, the start of the
+        // next band: only those draw-plane words are read (in flight with the window's
+        // rows), patched and written back
+        const int sh = base & 31, tb = base >> 5, tn = (tb + 1) & (NB - 1);
+        u32 oa[2], oc[2];
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            oa[q] = dp[tb * 128 + 64 * q];
+            oc[q] = sh ? dp[tn * 128 + 64 * q] : 0u;
+        }
         u32 P[32];
 #pragma unroll
         for (int i = 0; i < 32; i++) P[i] = i < nrows ? gb[((base + i) & (N - 1)) * RS] : 0u;
@@ -643,19 +663,16 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
             const int y = (int)((rows >> (8 * j)) & 0xFFu);
             if (y < N) rm |= 7u << (((y - base) & (N - 1)) - 1);
         }
-        // the window spans band tb from bit sh on and, when sh > 0, the start of the
-        // next band: only those words are read, patched and written back
-        const int sh = base & 31, tb = base >> 5, tn = (tb + 1) & (NB - 1);
         int dn = 0;                                     // eligible cells gained - lost
 #pragma unroll
         for (int q = 0; q < 2; q++) {
             const u32 ma = rm << sh, na = (geo.e[q] & rm) << sh;
-            const u32 a = dp[tb * 128 + 64 * q];
+            const u32 a = oa[q];
             dn += __builtin_popcount(na) - __builtin_popcount(a & ma);
             dp[tb * 128 + 64 * q] = (a & ~ma) | na;
             if (sh) {
                 const u32 mc = rm >> (32 - sh), nc = (geo.e[q] & rm) >> (32 - sh);
-                const u32 c = dp[tn * 128 + 64 * q];
+                const u32 c = oc[q];
                 dn += __builtin_popcount(nc) - __builtin_popcount(c & mc);
                 dp[tn * 128 + 64 * q] = (c & ~mc) | nc;
             }
