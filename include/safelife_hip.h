@@ -336,7 +336,9 @@ typedef struct sl_env_state {
                                  bit5 (128x128): the goals are the pool level's,
                                  as reset (set by the reset, cleared by the first
                                  change): their colours come from the pool's
-                                 goal_planes.
+                                 goal_planes; bit6 (128x128): board_planes hold
+                                 the board; bit7: with bit6, the uint16 board
+                                 is complete too (else only its band-edge rows).
                                  Anything
                                  that writes the goals other than the 64x64
                                  kernel and its reset clears it.               */
@@ -351,6 +353,20 @@ typedef struct sl_env_state {
                                  with those whose uniforms spawn, before the
                                  step kernel runs.  Or NULL (the step kernel
                                  then ranks and draws itself)                  */
+    uint32_t *board_planes;   /* 128x128, or NULL: [B,4,32,64] u32 in the goals
+                                 mirror's layout ([b][t][q][lane], word q =
+                                 plane q & 15 of column 2 lane + (q >> 4), rows
+                                 32t..32t+31).  When set, a Philox step of the
+                                 fast kernel without obs_out or capture keeps
+                                 the board here (planes_ok bit6) and writes of
+                                 the uint16 board only its band-edge rows (32t,
+                                 32t + 31) and the cells the action and exits
+                                 edit: bit7 then says the uint16 board is
+                                 complete.  sl_env_board_sync completes it; the
+                                 library's other entry points that read or
+                                 write st->board do so themselves.  A caller
+                                 that writes the uint16 board clears planes_ok
+                                 (as for the goals mirror).                    */
 } sl_env_state;
 
 /* A device-resident level pool (the level_iterator's levels). */
@@ -487,6 +503,11 @@ int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const int32_t *acti
                 const sl_env_cfg *cfg, double *reward, uint8_t *done,
                 uint8_t *info_flags, int32_t *ep_len, int32_t *ep_reward,
                 void *stream);
+
+/* Complete the uint16 board of every env whose board lives in st->board_planes
+ * (planes_ok bit6 without bit7): needed before reading st->board directly after
+ * steps that kept the board in planes.  No-op without board_planes. */
+int sl_env_board_sync(sl_env_state *st, void *stream);
 
 /* Reset the envs with mask[b] != 0 (mask NULL = all) from `pool`. */
 int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const uint8_t *mask,

@@ -38,6 +38,7 @@
 // Finished envs are queued and reset by a follow-up kernel (k_env_reset_list_wide,
 // one 1024-thread block per env).
 #include "sl_bits.h"
+#include "sl_env_action.h"
 
 using namespace sl;
 using namespace sl::fast;
@@ -434,7 +435,17 @@ k_env_step_bits128(Step128KArgs ka) {
     const u32 *gp = (roll >= 0 && (gok & 32) && pool.goal_planes)
                         ? pool.goal_planes + (int64_t)rec(V, R_LI) * (3 * NB * N) : nullptr;
     int pts = 0, scr = 0, pos = 0, side = 0;
-    u32 up = gb[(N - 1) * RS], row0 = 0;
+    // plane mode (fx.plane_mode, Philox only): the board lives in st.board_planes, in
+    // the mirror's layout; pin = this env's planes hold it (planes_ok bit 6; else this
+    // step reads the uint16 board and writes every plane word).  Of the uint16 board
+    // only the band-edge rows 32t and 32t + 31 are kept, for the halos
+    const bool pmode = MODE == SPAWN_PHILOX && fx.plane_mode;
+    const bool pin = pmode && (pok_all & 64);
+    const LanePtr<u32> bpl{pmode ? st.board_planes + b * (int64_t)(NB * MW) : nullptr};
+    // ... and the rows agent_y - 2 .. agent_y + 2, which the next step's action reads
+    // (k_env_action_planes128: the cells it can touch lie within them)
+    const int agy = __builtin_amdgcn_readfirstlane(rec(V, R_AY));
+    u32 up = gb[(N - 1) * RS], row0 = pin ? gb[0] : 0u;
     // SPAWN_DECIDED: the eligibility planes of the previous band (of band 0 in LDS, in
     // the draw slots this mode does not use), the advanced row 31 of the band before
     // that and row 0 of band 1: band t - 1's next eligibility is evaluated once band t
@@ -448,14 +459,37 @@ k_env_step_bits128(Step128KArgs ka) {
 #pragma unroll 1
     for (int t = 0; t < NB; t++) {
         u32 P[32];
-        load_pairs_nt<RS>(gb + 32 * t * RS, P);
+        u32 last;
+        if (pin) {
+#pragma unroll
+            for (int k = 0; k < 32; k++) P[k] = __builtin_nontemporal_load(&bpl[t * MW + k * 64]);
+            last = gb[(32 * t + 31) * RS];     // (this band's edge store comes after)
+        } else {
+            load_pairs_nt<RS>(gb + 32 * t * RS, P);
+        }
         const u32 dn = t < NB - 1 ? gb[(32 * t + 32) * RS] : row0;
         wait_lgkm();            // the previous band's reads of the buffer are done
         if (roll >= 0) pool_dma128(pp, t, sdy, lane_now(), spool);
         else start_band_lds(gs + 32 * t * RS, lane_now(), spool);
-        if (t == 0) row0 = P[0];
-        const u32 last = P[31];
-        transpose32(P);
+        if (!pin) {
+            if (t == 0) row0 = P[0];
+            last = P[31];
+            transpose32(P);
+        }
+        // planes a birth or death clears but never sets: whether any changed cell
+        // held one (their words are then stored too)
+        u32 oth[2] = {0u, 0u};
+        if (pin) {
+#pragma unroll
+            for (int w = 0; w < 2; w++) {
+                u32 o = PL(P, 1, w) | PL(P, 2, w);
+#pragma unroll
+                for (int k = 4; k <= 8; k++) o |= PL(P, k, w);
+#pragma unroll
+                for (int k = 12; k <= 15; k++) o |= PL(P, k, w);
+                oth[w] = o;
+            }
+        }
         u32 cb[2];
         GeoBand<MODE> geo{lane_now(), 32 * t, HaloView{up, t < NB - 1 ? dn : row0}, ssrc, pos_b, 0, 0, slots};
         if (MODE == SPAWN_DECIDED) draw_planes(geo, me, 0, t, dfl & 1);
@@ -511,14 +545,66 @@ k_env_step_bits128(Step128KArgs ka) {
         pos += r;
         side += e;
         const u32 rb = wave_or(cb[0] | cb[1]);
-        if (rb) {
-            // only the changed rows, whole (a wave-uniform branch per row; the 64-byte
-            // sector masks of the goals' stores measured 1.3% slower here, where
-            // nearly every sector of a changed row changes)
-            transpose32(P);
+        if (pin) {
+            // the plane words a change can alter: alive, destructible and colours
+            // (births set them, deaths clear them); the others only when a changed
+            // cell held one of them.  Then the band's edge rows, packed from the planes
+            if (rb) {
 #pragma unroll
-            for (int y = 0; y < 32; y++)
-                if ((rb >> y) & 1u) __builtin_nontemporal_store(P[y], &gb[(32 * t + y) * RS]);
+                for (int w = 0; w < 2; w++) {
+                    __builtin_nontemporal_store(PL(P, 0, w), &bpl[t * MW + (0 + 16 * w) * 64]);
+                    __builtin_nontemporal_store(PL(P, 3, w), &bpl[t * MW + (3 + 16 * w) * 64]);
+#pragma unroll
+                    for (int k = 9; k <= 11; k++)
+                        __builtin_nontemporal_store(PL(P, k, w), &bpl[t * MW + (k + 16 * w) * 64]);
+                }
+                if (wave_or((oth[0] & cb[0]) | (oth[1] & cb[1]))) {
+#pragma unroll
+                    for (int k = 0; k < 32; k++) {
+                        const int pl = k & 15;
+                        if (pl != 0 && pl != 3 && (pl < 9 || pl > 11))
+                            __builtin_nontemporal_store(P[k], &bpl[t * MW + k * 64]);
+                    }
+                }
+                if (rb & 1u) {          // row 32t: bit 0 of every plane word
+                    u32 r = 0u;
+#pragma unroll
+                    for (int k = 0; k < 32; k++) r = __builtin_amdgcn_alignbit(P[k], r, 1);
+                    __builtin_nontemporal_store(r, &gb[(32 * t) * RS]);
+                }
+                if (rb >> 31) {         // row 32t + 31: bit 31 of every plane word
+                    u32 r = 0u;
+#pragma unroll
+                    for (int k = 31; k >= 0; k--) r = __builtin_amdgcn_alignbit(r, P[k], 31);
+                    __builtin_nontemporal_store(r, &gb[(32 * t + 31) * RS]);
+                }
+            }
+            // the rows round the agent, changed or not (they may be stale from steps
+            // with the agent elsewhere)
+#pragma unroll 1
+            for (int d = -2; d <= 2; d++) {
+                const int y = (agy + d) & (N - 1);
+                if ((y >> 5) != t) continue;
+                const u32 yr = (u32)(y & 31);
+                u32 r = 0u;
+#pragma unroll
+                for (int k = 0; k < 32; k++) r |= ((P[k] >> yr) & 1u) << k;
+                __builtin_nontemporal_store(r, &gb[y * RS]);
+            }
+        } else {
+            if (pmode) {        // into plane mode: every plane word, and the rows below
+#pragma unroll
+                for (int k = 0; k < 32; k++) __builtin_nontemporal_store(P[k], &bpl[t * MW + k * 64]);
+            }
+            if (rb) {
+                // only the changed rows, whole (a wave-uniform branch per row; the 64-byte
+                // sector masks of the goals' stores measured 1.3% slower here, where
+                // nearly every sector of a changed row changes)
+                transpose32(P);
+#pragma unroll
+                for (int y = 0; y < 32; y++)
+                    if ((rb >> y) & 1u) __builtin_nontemporal_store(P[y], &gb[(32 * t + y) * RS]);
+            }
         }
     }
     if (MODE == SPAWN_DECIDED) {
@@ -532,7 +618,9 @@ k_env_step_bits128(Step128KArgs ka) {
     const int possible = wave_total(pos), side_total = wave_total(side);
     // goals mirror bits, and bit 3 = the board's draw planes hold the advanced board's
     // eligible cells (decided replay only: any other step clears it)
-    const int ok = gok | (me.base ? 8 : 0);
+    // bit 6: the planes hold the board; bit 7: so does the whole uint16 board (a step
+    // into plane mode stored its changed rows as well)
+    const int ok = gok | (me.base ? 8 : 0) | (pmode ? (pin ? 64 : 64 | 128) : 0);
     if (ok != pok_all && lane_now() == 0) st.planes_ok[b] = ok;
     // the epilogue's inputs, loaded now (in flight with the row stores) rather than held
     // through the bands: the reward, the bonus term and the record again (L2)
@@ -546,6 +634,8 @@ k_env_step_bits128(Step128KArgs ka) {
                                              k.a.bonus_period, k.a.bonus_len)];
     wait_vm();              // row stores land before the epilogue rewrites the exits
     if (lane_now() == 0) {
+        // (plane mode: the exits' colour is kept in the uint16 cells only -- no rule,
+        // score or action term reads an exit's colour, and k_board_sync128 keeps them)
         const bool reset = epilogue_core(k.st, k.a, b, fl, act_reward, points, score, possible,
                                          side_total, k.reward_out, k.done_out, k.flags_out,
                                          k.ep_len_out, k.ep_rew_out);
@@ -959,12 +1049,120 @@ k_stream_draw128_bits(Step128KArgs ka) {
     }
 }
 
+// ---- board planes (sl_env_state.board_planes, plane mode)
+// k_env_action for a plane-mode step (one lane per env): an env whose board is in
+// planes (planes_ok bit 6) reads the cells its action can touch from the uint16 board
+// -- the step kernel keeps the rows round the agent whole -- and each edit goes to
+// the uint16 cell and to the planes (XOR of its changed bits; one bit-per-plane XOR
+// atomic per changed bit measured 31 vs 9 us per launch for the uint16 action).
+// Other envs take the uint16 action (env_action_one).
+__global__ void __launch_bounds__(256)
+k_env_action_planes128(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int ctc,
+                       int64_t *__restrict__ act) {
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= st.B) return;
+    if (!(st.planes_ok[b] & 64)) {
+        env_action_one<false>(st, actions, ctp, ctc, act, b);
+        return;
+    }
+    u32 *bp = st.board_planes + b * (int64_t)(NB * MW);
+    uint16_t *bd = st.board + b * (int64_t)(N * N);
+    const int a = actions[b];
+    fast::GlobalEnv e{st, b};
+    fast::OverlayT<fast::GlobalCells> ov;
+    ov.src.bd = bd;
+    ov.n = 0;
+    const int reward = fast::act_core(e, a, N, N, ctp, ctc, ov);
+    // the edits into the planes: each edited cell's 16 plane words loaded together,
+    // the flips of every edit on the same words (cells of one column pair and band)
+    // applied to the first such edit's copy, which alone is stored (this lane owns the
+    // env's words: no atomics)
+    int key[4];
+    u32 W[4][16];
+    for (int k = 0; k < ov.n; k++) {
+        const int i = ov.idx[k], y = i >> 7, x = i & (N - 1);
+        key[k] = (y >> 5) * MW + (16 * (x & 1)) * 64 + (x >> 1);
+        bd[i] = (uint16_t)ov.val[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < ov.n) {
+#pragma unroll
+            for (int p = 0; p < 16; p++) W[k][p] = bp[key[k] + p * 64];
+        }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (k >= ov.n) continue;
+        bool first = true;
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+            if (m < k && key[m] == key[k]) first = false;
+        if (!first) continue;
+        u32 f[16];
+#pragma unroll
+        for (int p = 0; p < 16; p++) f[p] = 0u;
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            if (m < k || m >= ov.n || key[m] != key[k]) continue;
+            const int i = ov.idx[m];
+            const u32 d = ov.val[m] ^ ov.src(i), bit = 1u << ((i >> 7) & 31);
+#pragma unroll
+            for (int p = 0; p < 16; p++) f[p] |= ((d >> p) & 1u) ? bit : 0u;
+        }
+#pragma unroll
+        for (int p = 0; p < 16; p++)
+            if (f[p]) bp[key[k] + p * 64] = W[k][p] ^ f[p];
+    }
+    act[b] = reward;
+}
+
+// sl_env_board_sync / sync_board_planes: one wave per env
+__global__ void __launch_bounds__(64) k_board_sync128(sl_env_state st, int demote) {
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int pok = __builtin_amdgcn_readfirstlane(st.planes_ok[b]);
+    if (!(pok & 64)) return;
+    if (!(pok & 128)) {
+        // the exit cells hold their colour in the uint16 board only (the epilogue
+        // writes them): read before the rows are rewritten, put back after
+        uint16_t *cells = st.board + b * (int64_t)(N * N);
+        const int ne = min(__builtin_amdgcn_readfirstlane(st.exit_count[b]), SL_MAX_EXITS);
+        int ei = -1;
+        uint16_t ev = 0;
+        if (lane < ne) {
+            ei = st.exit_y[b * SL_MAX_EXITS + lane] * N + st.exit_x[b * SL_MAX_EXITS + lane];
+            ev = cells[ei];
+        }
+        wait_vm();
+        const u32 *bp = st.board_planes + b * (int64_t)(NB * MW) + lane;
+        u32 *gb = reinterpret_cast<u32 *>(st.board + b * (int64_t)(N * N)) + lane;
+#pragma unroll 1
+        for (int t = 0; t < NB; t++) {
+            u32 P[32];
+#pragma unroll
+            for (int k = 0; k < 32; k++) P[k] = bp[t * MW + k * 64];
+            transpose32(P);
+#pragma unroll
+            for (int y = 0; y < 32; y++) gb[(32 * t + y) * RS] = P[y];
+        }
+        wait_vm();
+        if (ei >= 0) cells[ei] = ev;
+    }
+    if (lane == 0) st.planes_ok[b] = demote ? pok & ~(64 | 128) : pok | 128;
+}
+
 }  // namespace
 
 namespace sl {
 
 bool bits128_shape(const sl_env_state &st) {
     return st.H == N && st.W == N && st.planes && st.planes_ok;
+}
+
+int sync_board_planes(const sl_env_state &st, int demote, hipStream_t s) {
+    if (!st.board_planes || !st.planes_ok || st.H != N || st.W != N || st.B <= 0) return SL_OK;
+    hipLaunchKernelGGL(k_board_sync128, dim3((unsigned)st.B), dim3(64), 0, s, st, demote);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
 int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
@@ -995,8 +1193,15 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
             hipLaunchKernelGGL(k_env_step_bits128<SPAWN_STREAM>, grid, dim3(64), 0, s, ka);
         }
     } else {
-        const int rc = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
-        if (rc) return rc;
+        if (fx.plane_mode) {
+            hipLaunchKernelGGL(k_env_action_planes128, dim3((unsigned)((st.B + 255) / 256)),
+                               dim3(256), 0, s, st, actions, ctp, ctc,
+                               scratch_of(fx.scratch, st.B).act);
+            if (hipGetLastError() != hipSuccess) return SL_EHIP;
+        } else {
+            const int rc = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
+            if (rc) return rc;
+        }
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
         hipLaunchKernelGGL(k_env_step_bits128<SPAWN_PHILOX>, grid, dim3(64), 0, s, ka);
     }

@@ -1008,6 +1008,14 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     // their reset-list kernel, so they keep the list (and its per-parity lengths,
     // which only the reset-list kernel clears) going through captured steps.
     if (cap && small) fx.fuse_reset = 0;
+    // 128x128 board planes: a Philox step of the fast kernel without views or capture
+    // keeps the board in them; any other step first completes (and demotes) it
+    const bool planes128 = st->board_planes && st->planes_ok && st->H == 128 && st->W == 128;
+    fx.plane_mode = (fast128 && !replay && planes128 && !cfg->obs_out && !cap) ? 1 : 0;
+    if (planes128 && !fx.plane_mode) {
+        const int rc = sync_board_planes(*st, 1, s);
+        if (rc) return rc;
+    }
     // observations: packed views of 64x64 boards come out of the step kernel itself
     ObsArgs oa;
     if (cfg->obs_out) {
@@ -1144,9 +1152,16 @@ extern "C" int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_whi
                           void *stream) {
     if (!state_ok(st) || !out) return SL_EINVAL;
     ObsArgs a;
-    const int rc = obs_args(vh, vw, remove_white_goals, obs_mode, channels, nch, &a);
+    int rc = obs_args(vh, vw, remove_white_goals, obs_mode, channels, nch, &a);
+    if (rc) return rc;
+    rc = sync_board_planes(*st, 0, (hipStream_t)stream);
     if (rc) return rc;
     return launch_obs(*st, a, out, (hipStream_t)stream);
+}
+
+extern "C" int sl_env_board_sync(sl_env_state *st, void *stream) {
+    if (!state_ok(st)) return SL_EINVAL;
+    return sync_board_planes(*st, 0, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -1156,6 +1171,8 @@ extern "C" int sl_env_action(sl_env_state *st, const int32_t *actions, int can_t
                              int can_toggle_colors, int64_t *act, void *stream) {
     if (!state_ok(st) || !actions || !act) return SL_EINVAL;
     if (st->B == 0) return SL_OK;
+    const int rc = sync_board_planes(*st, 1, (hipStream_t)stream);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_env_action<true>, dim3((unsigned)((st->B + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, *st, actions, can_toggle_powers, can_toggle_colors,
                        act);
@@ -1172,6 +1189,8 @@ extern "C" int sl_env_advance(sl_env_state *st, const sl_env_cfg *cfg, void *str
     const int64_t B = st->B;
     if (B == 0) return SL_OK;
     hipStream_t s = (hipStream_t)stream;
+    const int rcs = sync_board_planes(*st, 1, s);
+    if (rcs) return rcs;
     const Scratch sc = scratch_of(cfg->scratch, B);
     const size_t lds = (size_t)2 * st->H * st->W * sizeof(uint16_t);
     StepArgs a{};
@@ -1213,6 +1232,8 @@ extern "C" int sl_env_advance(sl_env_state *st, const sl_env_cfg *cfg, void *str
 extern "C" int sl_env_rescore(sl_env_state *st, int32_t *points, void *stream) {
     if (!state_ok(st)) return SL_EINVAL;
     if (st->B == 0) return SL_OK;
+    const int rc = sync_board_planes(*st, 0, (hipStream_t)stream);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_env_rescore, dim3((unsigned)st->B), dim3(NT), 0, (hipStream_t)stream,
                        *st, points);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
@@ -1221,6 +1242,8 @@ extern "C" int sl_env_rescore(sl_env_state *st, int32_t *points, void *stream) {
 extern "C" int sl_env_exit_colors(sl_env_state *st, int mode, void *stream) {
     if (!state_ok(st) || (mode != 0 && mode != 1)) return SL_EINVAL;
     if (st->B == 0) return SL_OK;
+    const int rc = sync_board_planes(*st, 1, (hipStream_t)stream);
+    if (rc) return rc;
     hipLaunchKernelGGL(k_env_exit_colors, dim3((unsigned)((st->B + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, *st, mode);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;

@@ -124,7 +124,7 @@ __device__ __forceinline__ bool epilogue_core(const sl_env_state &st, const Step
                                               int score, int possible, int side,
                                               double *reward_out, uint8_t *done_out,
                                               uint8_t *flags_out, int32_t *ep_len_out,
-                                              int32_t *ep_rew_out) {
+                                              int32_t *ep_rew_out, int *can_out = nullptr) {
     const int W = st.W;
     uint16_t *gb = st.board + b * (int64_t)st.H * W;
     const int r_int = act_reward + (points - f.old_points());
@@ -138,6 +138,7 @@ __device__ __forceinline__ bool epilogue_core(const sl_env_state &st, const Step
     st.possible[b] = possible;
     const bool can = can_exit_now(f.min_performance(), score, f.baseline(), possible);
     const uint16_t ev = (uint16_t)(LEVEL_EXIT | (can ? COLOR_R : 0u));
+    if (can_out) *can_out = can ? 1 : 0;
     const int ne = min(f.exit_count(), SL_MAX_EXITS);
     for (int e = 0; e < ne; e++)      // exits are frozen and never change otherwise
         gb[f.exit_y(e) * W + f.exit_x(e)] = ev;
@@ -346,6 +347,8 @@ struct FastExtra {
     const int64_t *stream_base;   // *stream_base + the step
     const sl_mt19937 *mt;   // replay from the device generator (sl_env_cfg.mt) or NULL:
                             // stream_offsets fills its ring for the step's range
+    int32_t plane_mode = 0; // 128x128 Philox without views or capture, board_planes set:
+                            // the board is kept in sl_env_state.board_planes
 };
 // replay-mode phases of a bit-sliced launcher: whether it runs the action + count
 // prologue, and whether it continues past the offsets scan to the step kernel
@@ -377,6 +380,10 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
                         uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s);
 // the action of every env (k_env_action, one lane per env): state and cell edits in
 // HBM, reward into act[b]; the 128x128 kernel's pre-pass (sl_env.hip)
+// 128x128 board planes (sl_env_state.board_planes): complete the uint16 board of envs
+// kept in planes; demote: then mark the planes stale (before a step or edit that
+// works on the uint16 board).  No-op unless the state has board planes.
+int sync_board_planes(const sl_env_state &st, int demote, hipStream_t s);
 int launch_env_action(const sl_env_state &st, const int32_t *actions, int ctp, int ctc,
                       int64_t *act, hipStream_t s);
 // resets of the envs queued in the scratch list for step `step`, one 1024-thread

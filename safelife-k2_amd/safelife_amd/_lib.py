@@ -43,7 +43,7 @@ class EnvState(ctypes.Structure):
                 ("exit_count", vp), ("exit_y", vp), ("exit_x", vp),
                 ("level_index", vp), ("episodes", vp), ("num_steps", vp),
                 ("spawn_flags", vp), ("start_roll", vp), ("planes", vp), ("planes_ok", vp),
-                ("elig_planes", vp)]
+                ("elig_planes", vp), ("board_planes", vp)]
 
 
 class LevelPool(ctypes.Structure):
@@ -133,7 +133,8 @@ def lib():
     game = {"sl_env_action": [ctypes.POINTER(EnvState), vp, ctypes.c_int, ctypes.c_int, vp, vp],
             "sl_env_advance": [ctypes.POINTER(EnvState), ctypes.POINTER(EnvCfg), vp],
             "sl_env_rescore": [ctypes.POINTER(EnvState), vp, vp],
-            "sl_env_exit_colors": [ctypes.POINTER(EnvState), ctypes.c_int, vp]}
+            "sl_env_exit_colors": [ctypes.POINTER(EnvState), ctypes.c_int, vp],
+            "sl_env_board_sync": [ctypes.POINTER(EnvState), vp]}
     for name, args in game.items():
         # (an A/B build of an older revision, SAFELIFE_HIP_LIB, may lack these)
         if hasattr(L, name) or LIB_PATH == _DEFAULT_LIB:

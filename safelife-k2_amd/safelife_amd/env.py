@@ -132,8 +132,9 @@ class SafeLifeGame:
         self._venv.board[self._idx].copy_(self._upload(value))
         self._set("spawn_flags", self._st("spawn_flags") | 1)   # may now hold a spawner
         self._venv._may_spawn = True
-        # bit 3: the board's draw planes (128x128 replay) described the old board
-        self._venv.planes_ok[self._idx].bitwise_and_(~8)
+        # bit 3: the board's draw planes (128x128 replay) described the old board;
+        # bits 6-7: the board's bit planes (sl_env_state.board_planes) are stale
+        self._venv.planes_ok[self._idx].bitwise_and_(~(8 | 64 | 128))
         self.rescore()
 
     @property
@@ -552,6 +553,7 @@ class SafeLifeEnv:
             t = torch.from_numpy(np.ascontiguousarray(board, dtype=np.uint16)).to(v.device)
             keep.append(t)
             s.board = t.data_ptr()
+            s.board_planes = None       # (the env's own planes describe its own board)
         if goals is not None:
             t = torch.from_numpy(np.ascontiguousarray(goals, dtype=np.uint16)).to(v.device)
             keep.append(t)

@@ -157,7 +157,8 @@ class SafeLifeVecEnv:
     def _alloc(self, obs_dtype):
         torch, dev, B, H, W = self.torch, self.device, self.B, self.H, self.W
         z = lambda *s, dt=torch.int32: torch.zeros(s, dtype=dt, device=dev)
-        self.board = z(B, H, W, dt=torch.uint16)
+        self._board = z(B, H, W, dt=torch.uint16)
+        self._board_stale = False
         self.goals = z(B, H, W, dt=torch.uint16)
         self.start_board = z(B, H, W, dt=torch.uint16)
         self.st_t = {
@@ -175,7 +176,7 @@ class SafeLifeVecEnv:
         }
         s = _lib.EnvState()
         s.B, s.H, s.W = B, H, W
-        s.board, s.goals, s.start_board = (self.board.data_ptr(), self.goals.data_ptr(),
+        s.board, s.goals, s.start_board = (self._board.data_ptr(), self.goals.data_ptr(),
                                            self.start_board.data_ptr())
         for k, t in self.st_t.items():
             setattr(s, k, t.data_ptr())
@@ -186,6 +187,13 @@ class SafeLifeVecEnv:
             self.planes = z(B, H // 32, 32, 64)
             s.planes = self.planes.data_ptr()
             s.planes_ok = self.planes_ok.data_ptr()
+        self.board_planes = None
+        if (H, W) == (128, 128) and self.rng == "philox":
+            # the 128x128 board in bit planes, kept there by Philox steps without
+            # observations (sl_env_state.board_planes); `board` completes the uint16
+            # tensor when it is read
+            self.board_planes = z(B, H // 32, 32, 64)
+            s.board_planes = self.board_planes.data_ptr()
         if (H, W) == (128, 128) and self.rng == "stream":
             # replay's draw planes: each tensor's eligible cells, then its decided
             # spawns (4 KiB per env)
@@ -238,6 +246,7 @@ class SafeLifeVecEnv:
         # running episodes' start boards are no longer levels of the pool: the
         # kernels read them from HBM until those envs are reset from the new pool
         self.st_t["start_roll"].fill_(-1)
+        self._board_stale = False      # (planes_ok is zeroed: the uint16 board holds)
 
     # ------------------------------------------------- the device generator's ring
     @staticmethod
@@ -484,6 +493,8 @@ class SafeLifeVecEnv:
             cfg.stream_phase = 2
             cfg.stream_base = self._stream_base.data_ptr()
         launch()
+        if self.board_planes is not None:
+            self._board_stale = True
         self._step_index += 1
         self.global_counter.num_steps += self.B
         if self.mt is not None and self._step_index % self.STREAM_CHECK_EVERY == 0:
@@ -661,9 +672,32 @@ class SafeLifeVecEnv:
         return s
 
     def _state_tensor(self, name):
-        if name in ("board", "goals", "start_board", "planes", "planes_ok", "elig_planes"):
+        if name == "board":
+            return self._board
+        if name in ("goals", "start_board", "planes", "planes_ok", "elig_planes", "board_planes"):
             return getattr(self, name)
         return self.st_t[name]
+
+    @property
+    def board(self):
+        """uint16 [B, H, W] boards.  A 128x128 batch stepped without observations keeps
+        its boards in bit planes (sl_env_state.board_planes); reading this completes
+        the tensor first (sl_env_board_sync, stream-ordered).  Write boards through
+        set_state / load_state_dict (or clear planes_ok after writing)."""
+        if self._board_stale:
+            self.sync_board()
+        return self._board
+
+    def sync_board(self):
+        """Complete the uint16 boards of envs whose board lives in planes (no-op
+        otherwise; no host sync)."""
+        self._board_stale = False
+        L = _lib.lib()
+        # (an A/B build of an older revision, SAFELIFE_HIP_LIB, has no board planes)
+        if self.board_planes is not None and hasattr(L, "sl_env_board_sync"):
+            _lib.check(L.sl_env_board_sync(ctypes.byref(self._state),
+                                           _lib.stream_ptr(self.device)),
+                       "sl_env_board_sync")
 
     @property
     def state(self):
@@ -678,7 +712,7 @@ class SafeLifeVecEnv:
     def set_state(self, board, goals, start_board, **scalars):
         """Load explicit state (for tests / checkpoints).  Arrays are [B,...]."""
         torch = self.torch
-        for dst, src in ((self.board, board), (self.goals, goals), (self.start_board, start_board)):
+        for dst, src in ((self._board, board), (self.goals, goals), (self.start_board, start_board)):
             dst.copy_(torch.as_tensor(np.ascontiguousarray(src, dtype=np.uint16)).to(self.device))
         for k, v in scalars.items():
             t = self.st_t[k]
@@ -690,6 +724,7 @@ class SafeLifeVecEnv:
         longer match pool levels (kernels read them from HBM), the bit-plane
         mirrors are stale and the reset lists start empty."""
         self.st_t["start_roll"].fill_(-1)
+        self._board_stale = False      # (planes_ok is zeroed: the uint16 board holds)
         # may hold spawners (replay counts them); bit 2 (128x128 boards): the start board
         # uses cell bits 12-14, which the 128x128 kernel then compares in a second pass
         hi = start_board_hi_bits(self.start_board) & ((self.H, self.W) == (128, 128))
@@ -723,7 +758,7 @@ class SafeLifeVecEnv:
             import warnings
             warnings.warn("state_dict level_index outside the current pool of %d levels"
                           " (informational only)" % self.pool.K)
-        self.board.copy_(d["board"])
+        self._board.copy_(d["board"])
         self.goals.copy_(d["goals"])
         self.start_board.copy_(d["start_board"])
         for k, v in self.st_t.items():

@@ -1,0 +1,151 @@
+"""The 128x128 board kept in bit planes (sl_env_state.board_planes, round 5).
+
+A Philox step of the fast kernel without views or capture keeps the board in planes
+and writes only the band-edge rows of the uint16 board; every reader completes it
+first (SafeLifeVecEnv.board, sl_env_obs, the game-level entry points).  These tests
+run one batch with planes and one without side by side from the same seed and require
+identical outputs, through the transitions: into plane mode after resets, board reads
+between plane steps (uint16 complete, planes still authoritative), observations, a
+step with views (back to the uint16 board), set_state.  The planes themselves are
+checked against the completed board.  The C5 every-env and bench-regime tests
+(test_gpu_headline.py, test_gpu_bench_regime.py) run the plane path against the
+oracle at full batch.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+POOLS = os.path.join(os.path.dirname(__file__), "golden", "pools")
+C5 = os.path.join(POOLS, "c5_navigation_128.npz")
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    import safelife_amd  # noqa: F401
+    return torch, torch.device("cuda:0")
+
+
+def _pair(torch_dev, B, seed, tl):
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    torch, dev = torch_dev
+    kw = dict(time_limit=tl, view_shape=(33, 33), penalty_coef=1.0, min_performance=0.01,
+              rng="philox", seed=seed, level_order="random", augment_roll=True,
+              kernel="fast", compute_obs=False)
+    a = SafeLifeVecEnv(LevelPool.load(C5), B, dev, **kw)
+    b = SafeLifeVecEnv(LevelPool.load(C5), B, dev, **kw)
+    b._state.board_planes = None         # the uint16-only form
+    b.board_planes = None
+    a.reset()
+    b.reset()
+    assert a.board_planes is not None
+    return a, b
+
+
+def _host_planes(board):
+    """[128, 128] uint16 -> [4, 32, 64] uint32 in board_planes' layout: word k of
+    lane j in band t holds bit k & 15 of column 2 j + (k >> 4), rows 32 t + r at bit r."""
+    b = board.astype(np.uint32).reshape(4, 32, 64, 2)          # [t, r, j, q]
+    out = np.zeros((4, 32, 64), np.uint64)
+    sh = np.arange(32, dtype=np.uint64)[None, :, None]
+    for k in range(32):
+        bits = ((b[:, :, :, k >> 4] >> (k & 15)) & 1).astype(np.uint64)
+        out[:, k, :] = (bits << sh).sum(axis=1)
+    return out.astype(np.uint32)
+
+
+def _same_state(a, b, ctx):
+    assert np.array_equal(a.board.cpu().numpy(), b.board.cpu().numpy()), ctx
+    assert np.array_equal(a.goals.cpu().numpy(), b.goals.cpu().numpy()), ctx
+    for k in a.st_t:
+        assert np.array_equal(a.st_t[k].cpu().numpy(), b.st_t[k].cpu().numpy()), (ctx, k)
+
+
+def test_plane_mode_matches_uint16_mode(torch_dev):
+    torch, dev = torch_dev
+    B, T = 512, 48
+    a, b = _pair(torch_dev, B, seed=99, tl=12)
+    rng = np.random.RandomState(5)
+    obs_a = torch.zeros_like(a.obs)
+    obs_b = torch.zeros_like(b.obs)
+    n_done = 0
+    for t in range(T):
+        acts = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+        if t in (17, 18):          # steps with views: the uint16 board, then back
+            a.step_async(acts, obs_out=obs_a)
+            b.step_async(acts, obs_out=obs_b)
+            assert torch.equal(obs_a, obs_b), t
+        else:
+            a.step_async(acts)
+            b.step_async(acts)
+        for x, y in ((a.reward, b.reward), (a.done, b.done), (a.flags, b.flags),
+                     (a.ep_len, b.ep_len), (a.ep_rew, b.ep_rew)):
+            assert torch.equal(x, y), t
+        n_done += int(b.done.sum().item())
+        if t % 7 == 3:             # a read between plane steps
+            _same_state(a, b, t)
+        if t == 10:
+            assert torch.equal(a.observe(), b.observe()), t
+        if t == 30:                # explicit state: the next step goes into plane mode
+            a.set_state(b.board.cpu().numpy(), b.goals.cpu().numpy(),
+                        b.start_board.cpu().numpy())
+            b.set_state(b.board.cpu().numpy(), b.goals.cpu().numpy(),
+                        b.start_board.cpu().numpy())
+    assert n_done >= B
+    _same_state(a, b, "end")
+    # the planes are the board (envs whose board lives in planes)
+    pok = a.planes_ok.cpu().numpy()
+    assert ((pok & 64) != 0).sum() > B // 2
+    bd = a.board.cpu().numpy()
+    bp = a.board_planes.cpu().numpy().view(np.uint32)
+    for e in np.nonzero(pok & 64)[0][:64]:
+        hp, dp = _host_planes(bd[e]), bp[e].copy()
+        # an exit's colour is kept in the uint16 cell only (nothing reads it from planes)
+        for y, x in zip(*np.nonzero(bd[e] & 0x100)):
+            k = 9 + 16 * (x & 1)
+            hp[y >> 5, k, x >> 1] &= ~np.uint32(1 << (y & 31))
+            dp[y >> 5, k, x >> 1] &= ~np.uint32(1 << (y & 31))
+        assert np.array_equal(dp, hp), e
+
+
+def test_plane_mode_full_batch_reads_only_at_end(torch_dev):
+    """65 536 envs, 20 steps of plane mode with no read in between (every env crosses
+    an episode end): the same as the uint16 form, outputs every step, state at the end."""
+    torch, dev = torch_dev
+    B, T = 65536, 20
+    a, b = _pair(torch_dev, B, seed=7, tl=8)
+    rng = np.random.RandomState(9)
+    for t in range(T):
+        acts = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+        a.step_async(acts)
+        b.step_async(acts)
+        assert torch.equal(a.reward, b.reward) and torch.equal(a.done, b.done), t
+    _same_state(a, b, "end")
+
+
+def test_game_entries_complete_the_board(torch_dev):
+    """The game-level entry points on a batch kept in planes read and write the
+    completed board: sl_env_rescore's points equal the uint16 form's."""
+    import ctypes
+    from safelife_amd import _lib
+    torch, dev = torch_dev
+    B = 64
+    a, b = _pair(torch_dev, B, seed=3, tl=50)
+    rng = np.random.RandomState(2)
+    for t in range(6):
+        acts = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+        a.step_async(acts)
+        b.step_async(acts)
+    L = _lib.lib()
+    pa = torch.zeros(B, dtype=torch.int32, device=dev)
+    pb = torch.zeros(B, dtype=torch.int32, device=dev)
+    # through the C entry directly (no Python-side sync first)
+    _lib.check(L.sl_env_rescore(ctypes.byref(a._state), pa.data_ptr(), _lib.stream_ptr(dev)),
+               "sl_env_rescore")
+    _lib.check(L.sl_env_rescore(ctypes.byref(b._state), pb.data_ptr(), _lib.stream_ptr(dev)),
+               "sl_env_rescore")
+    assert torch.equal(pa, pb)
+    a._board_stale = False               # (the entry completed it)
+    assert torch.equal(a._board, b.board)
