@@ -442,9 +442,13 @@ k_env_step_bits128(Step128KArgs ka) {
     const bool pmode = MODE == SPAWN_PHILOX && fx.plane_mode;
     const bool pin = pmode && (pok_all & 64);
     const LanePtr<u32> bpl{pmode ? st.board_planes + b * (int64_t)(NB * MW) : nullptr};
-    // ... and the rows agent_y - 2 .. agent_y + 2, which the next step's action reads
-    // (k_env_action_planes128: the cells it can touch lie within them)
+    // ... and the cells round the agent the next step's action reads
+    // (k_env_action_planes128: row agent_y, column agent_x in rows agent_y +- 1, 2)
     const int agy = __builtin_amdgcn_readfirstlane(rec(V, R_AY));
+    const int agx = __builtin_amdgcn_readfirstlane(rec(V, R_AX));
+    // the cells this step's action edited in the uint16 board (k_env_action_planes128)
+    const uint64_t ecells = pin ? (uint64_t)w.act[st.B + b] : ~0ull;
+    const uint64_t evals = pin ? (uint64_t)w.act[2 * st.B + b] : 0ull;
     u32 up = gb[(N - 1) * RS], row0 = pin ? gb[0] : 0u;
     // SPAWN_DECIDED: the eligibility planes of the previous band (of band 0 in LDS, in
     // the draw slots this mode does not use), the advanced row 31 of the band before
@@ -460,6 +464,8 @@ k_env_step_bits128(Step128KArgs ka) {
     for (int t = 0; t < NB; t++) {
         u32 P[32];
         u32 last;
+        bool patched = false;   // the action edited a cell of this band
+        u32 pk = 0u;            // plane words the action's edits changed (this lane)
         if (pin) {
 #pragma unroll
             for (int k = 0; k < 32; k++) P[k] = __builtin_nontemporal_load(&bpl[t * MW + k * 64]);
@@ -475,6 +481,29 @@ k_env_step_bits128(Step128KArgs ka) {
             if (t == 0) row0 = P[0];
             last = P[31];
             transpose32(P);
+        } else {
+            // the action's edits: those cells' values from the uint16 board, into the
+            // plane words of the lane holding each
+#pragma unroll 1
+            for (int m = 0; m < 4; m++) {
+                const int i = (int)((ecells >> (16 * m)) & 0xFFFFu);
+                if (i >= N * N || (i >> 12) != t) continue;
+                const int x = i & (N - 1);
+                const u32 d = (u32)(evals >> (16 * m)) & 0xFFFFu;      // the changed bits
+                const u32 yr = (u32)((i >> 7) & 31);
+                const bool mine = lane_now() == (x >> 1);
+                patched = true;
+                const u32 m2 = mine ? 1u << yr : 0u;
+                // branch-free (uniform per-plane branches here cost 50 us per launch)
+                const u32 m0 = (x & 1) ? 0u : m2, m1 = (x & 1) ? m2 : 0u;
+                pk |= mine ? d << (16 * (x & 1)) : 0u;
+#pragma unroll
+                for (int p = 0; p < 16; p++) {
+                    const u32 f = 0u - ((d >> p) & 1u);
+                    PL(P, p, 0) ^= m0 & f;
+                    PL(P, p, 1) ^= m1 & f;
+                }
+            }
         }
         // planes a birth or death clears but never sets: whether any changed cell
         // held one (their words are then stored too)
@@ -579,17 +608,38 @@ k_env_step_bits128(Step128KArgs ka) {
                     __builtin_nontemporal_store(r, &gb[(32 * t + 31) * RS]);
                 }
             }
-            // the rows round the agent, changed or not (they may be stale from steps
-            // with the agent elsewhere)
-#pragma unroll 1
-            for (int d = -2; d <= 2; d++) {
-                const int y = (agy + d) & (N - 1);
-                if ((y >> 5) != t) continue;
-                const u32 yr = (u32)(y & 31);
+            // the plane words the action's edits changed, in the lanes holding them
+            if (patched) {
+                const u32 pkw = wave_or(pk);
+#pragma unroll
+                for (int k = 0; k < 32; k++)
+                    if ((pkw >> k) & 1u)
+                        if ((pk >> k) & 1u) bpl[t * MW + k * 64] = P[k];
+            }
+            // the cells the next action can read (changed or not: they may be stale
+            // from steps with the agent elsewhere): row agy whole (moves left / right,
+            // toggles) and column agx in rows agy +- 1, 2 (moves up / down)
+            if ((agy >> 5) == t) {
+                const u32 yr = (u32)(agy & 31);
                 u32 r = 0u;
 #pragma unroll
                 for (int k = 0; k < 32; k++) r |= ((P[k] >> yr) & 1u) << k;
-                __builtin_nontemporal_store(r, &gb[y * RS]);
+                __builtin_nontemporal_store(r, &gb[agy * RS]);
+            }
+#pragma unroll 1
+            for (int d = -2; d <= 2; d++) {
+                const int y = (agy + d) & (N - 1);
+                if (d == 0 || (y >> 5) != t) continue;
+                const u32 yr = (u32)(y & 31);
+                u32 v = 0u;
+                if (agx & 1) {
+#pragma unroll
+                    for (int p = 0; p < 16; p++) v |= ((PL(P, p, 1) >> yr) & 1u) << p;
+                } else {
+#pragma unroll
+                    for (int p = 0; p < 16; p++) v |= ((PL(P, p, 0) >> yr) & 1u) << p;
+                }
+                if (lane_now() == (agx >> 1)) st.board[b * (int64_t)(N * N) + y * N + agx] = (uint16_t)v;
             }
         } else {
             if (pmode) {        // into plane mode: every plane word, and the rows below
@@ -1052,10 +1102,9 @@ k_stream_draw128_bits(Step128KArgs ka) {
 // ---- board planes (sl_env_state.board_planes, plane mode)
 // k_env_action for a plane-mode step (one lane per env): an env whose board is in
 // planes (planes_ok bit 6) reads the cells its action can touch from the uint16 board
-// -- the step kernel keeps the rows round the agent whole -- and each edit goes to
-// the uint16 cell and to the planes (XOR of its changed bits; one bit-per-plane XOR
-// atomic per changed bit measured 31 vs 9 us per launch for the uint16 action).
-// Other envs take the uint16 action (env_action_one).
+// -- the step kernel keeps them current (the agent's row, and its column two rows up
+// and down) -- and writes its edits there.  Other envs take the uint16 action
+// (env_action_one); an env with no scratch row list entry is then not in plane mode.
 __global__ void __launch_bounds__(256)
 k_env_action_planes128(sl_env_state st, const int32_t *__restrict__ actions, int ctp, int ctc,
                        int64_t *__restrict__ act) {
@@ -1065,7 +1114,6 @@ k_env_action_planes128(sl_env_state st, const int32_t *__restrict__ actions, int
         env_action_one<false>(st, actions, ctp, ctc, act, b);
         return;
     }
-    u32 *bp = st.board_planes + b * (int64_t)(NB * MW);
     uint16_t *bd = st.board + b * (int64_t)(N * N);
     const int a = actions[b];
     fast::GlobalEnv e{st, b};
@@ -1073,46 +1121,24 @@ k_env_action_planes128(sl_env_state st, const int32_t *__restrict__ actions, int
     ov.src.bd = bd;
     ov.n = 0;
     const int reward = fast::act_core(e, a, N, N, ctp, ctc, ov);
-    // the edits into the planes: each edited cell's 16 plane words loaded together,
-    // the flips of every edit on the same words (cells of one column pair and band)
-    // applied to the first such edit's copy, which alone is stored (this lane owns the
-    // env's words: no atomics)
-    int key[4];
-    u32 W[4][16];
-    for (int k = 0; k < ov.n; k++) {
-        const int i = ov.idx[k], y = i >> 7, x = i & (N - 1);
-        key[k] = (y >> 5) * MW + (16 * (x & 1)) * 64 + (x >> 1);
-        bd[i] = (uint16_t)ov.val[k];
-    }
+    // the edits go to the uint16 cells only; the cells (up to four 16-bit indices,
+    // 0xFFFF none) go to scratch act[B + b] and their changed bits to act[2B + b],
+    // which the step kernel flips in its planes.  (Writing the edits into the planes here --
+    // one XOR atomic per changed bit, or a read-modify-write of each edited cell's 16
+    // words -- cost 31 / 44 us per launch against 9 us for the uint16 action.)
+    uint64_t cells = ~0ull, vals = 0ull;
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-        if (k < ov.n) {
-#pragma unroll
-            for (int p = 0; p < 16; p++) W[k][p] = bp[key[k] + p * 64];
-        }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < 4; k++) {       // (static indices: the overlay stays in registers)
         if (k >= ov.n) continue;
-        bool first = true;
-#pragma unroll
-        for (int m = 0; m < 4; m++)
-            if (m < k && key[m] == key[k]) first = false;
-        if (!first) continue;
-        u32 f[16];
-#pragma unroll
-        for (int p = 0; p < 16; p++) f[p] = 0u;
-#pragma unroll
-        for (int m = 0; m < 4; m++) {
-            if (m < k || m >= ov.n || key[m] != key[k]) continue;
-            const int i = ov.idx[m];
-            const u32 d = ov.val[m] ^ ov.src(i), bit = 1u << ((i >> 7) & 31);
-#pragma unroll
-            for (int p = 0; p < 16; p++) f[p] |= ((d >> p) & 1u) ? bit : 0u;
-        }
-#pragma unroll
-        for (int p = 0; p < 16; p++)
-            if (f[p]) bp[key[k] + p * 64] = W[k][p] ^ f[p];
+        const int i = ov.idx[k];
+        const u32 v = ov.val[k], d = v ^ ov.src(i);    // (read before the cell is written)
+        if (!d) continue;
+        bd[i] = (uint16_t)v;
+        cells = (cells << 16) | (uint64_t)i;
+        vals = (vals << 16) | (uint64_t)d;
     }
+    act[st.B + b] = (int64_t)cells;
+    act[2 * st.B + b] = (int64_t)vals;
     act[b] = reward;
 }
 
