@@ -439,7 +439,7 @@ k_env_step_bits128(Step128KArgs ka) {
     // the mirror's layout; pin = this env's planes hold it (planes_ok bit 6; else this
     // step reads the uint16 board and writes every plane word).  Of the uint16 board
     // only the band-edge rows 32t and 32t + 31 are kept, for the halos
-    const bool pmode = MODE == SPAWN_PHILOX && fx.plane_mode;
+    const bool pmode = (MODE == SPAWN_PHILOX || MODE == SPAWN_DECIDED) && fx.plane_mode;
     const bool pin = pmode && (pok_all & 64);
     const LanePtr<u32> bpl{pmode ? st.board_planes + b * (int64_t)(NB * MW) : nullptr};
     // ... and the cells round the agent the next step's action reads
@@ -447,8 +447,9 @@ k_env_step_bits128(Step128KArgs ka) {
     const int agy = __builtin_amdgcn_readfirstlane(rec(V, R_AY));
     const int agx = __builtin_amdgcn_readfirstlane(rec(V, R_AX));
     // the cells this step's action edited in the uint16 board (k_env_action_planes128)
-    const uint64_t ecells = pin ? (uint64_t)w.act[st.B + b] : ~0ull;
-    const uint64_t evals = pin ? (uint64_t)w.act[2 * st.B + b] : 0ull;
+    // (replay: the count prologue has put them into the planes already)
+    const uint64_t ecells = (MODE == SPAWN_PHILOX && pin) ? (uint64_t)w.act[st.B + b] : ~0ull;
+    const uint64_t evals = (MODE == SPAWN_PHILOX && pin) ? (uint64_t)w.act[2 * st.B + b] : 0ull;
     u32 up = gb[(N - 1) * RS], row0 = pin ? gb[0] : 0u;
     // SPAWN_DECIDED: the eligibility planes of the previous band (of band 0 in LDS, in
     // the draw slots this mode does not use), the advanced row 31 of the band before
@@ -727,6 +728,33 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
     const StreamSrc none{nullptr, 0, nullptr};
     // the draw planes: each counted tensor's eligible cells, for k_stream_draw128
     u32 *dp = st.elig_planes ? st.elig_planes + b * kEligStride + kDrawPlanes + lane : nullptr;
+    // plane mode (sl_env_state.board_planes, planes_ok bit 6): the board is read from
+    // its planes -- only the four eligibility planes -- after the action's edits
+    // (k_env_action_planes128 wrote the uint16 cells, listed in act[3B + b]) have been
+    // put into them here, for this count and for the step kernel
+    const bool pm = ka.fx.plane_mode && st.board_planes && (rec(V, R_POK) & 64);
+    u32 *const bpw = pm ? st.board_planes + b * (int64_t)(NB * MW) : nullptr;
+    auto pload = [&](int t, int k) {       // (past the vector L1: the edits just stored)
+        return __hip_atomic_load(bpw + t * MW + k * 64 + lane, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (pm) {
+        const uint64_t ec = (uint64_t)w.act[3 * st.B + b];
+#pragma unroll 1
+        for (int m = 0; m < 4; m++) {
+            const int i = (int)((ec >> (16 * m)) & 0xFFFFu);
+            if (i >= N * N) continue;
+            if (lane < 16) {                 // lane p: plane p
+                const u32 v = st.board[off + i];
+                const int x = i & (N - 1);
+                const u32 bit = 1u << ((i >> 7) & 31);
+                u32 *wd = bpw + (i >> 12) * MW + (lane + 16 * (x & 1)) * 64 + (x >> 1);
+                const u32 o = __hip_atomic_load(wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *wd = ((v >> lane) & 1u) ? o | bit : o & ~bit;
+            }
+            wait_vm();
+        }
+    }
     auto keep = [&](const GeoBand<SPAWN_COUNT> &geo, int tensor, int t) {
         if (dp) {
             dp[(tensor * NB + t) * 128] = geo.e[0];
@@ -739,10 +767,18 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
 #pragma unroll 1
         for (int t = 0; t < NB; t++) {
             const int ru = (32 * t - 1) & (N - 1), rd = (32 * t + 32) & (N - 1);
-            const u32 up = g[ru * RS], dn = g[rd * RS];
+            const u32 up = g[ru * RS], dn = g[rd * RS];      // (band-edge rows: whole)
             u32 P[32];
-            load_pairs_nt<RS>(g + 32 * t * RS, P);
-            transpose32(P);
+            if (pm && tensor == 0) {
+#pragma unroll
+                for (int k = 0; k < 32; k++) {
+                    const int pl = k & 15;
+                    P[k] = (pl == 0 || pl == 4 || pl == 6 || pl == 7) ? pload(t, k) : 0u;
+                }
+            } else {
+                load_pairs_nt<RS>(g + 32 * t * RS, P);
+                transpose32(P);
+            }
             GeoBand<SPAWN_COUNT> geo{lane, 32 * t, HaloView{up, dn}, none, 0, 0, 0, nullptr};
             u32 ch[2];
             rule_planes(P, ch, geo, sc, 0u);
@@ -788,12 +824,25 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
             oc[q] = sh ? dp[tn * 128 + 64 * q] : 0u;
         }
         u32 P[32];
+        if (pm) {           // the window's rows straight from the planes of bands tb, tn
+            const u32 nm = nrows >= 32 ? 0xFFFFFFFFu : (1u << nrows) - 1u;
 #pragma unroll
-        for (int i = 0; i < 32; i++) P[i] = i < nrows ? gb[((base + i) & (N - 1)) * RS] : 0u;
-        transpose32(P);
+            for (int k = 0; k < 32; k++) {
+                const int pl = k & 15;
+                P[k] = 0u;
+                if (pl == 0 || pl == 4 || pl == 6 || pl == 7) {
+                    const u32 lo = pload(tb, k), hi = sh ? pload(tn, k) : 0u;
+                    P[k] = (sh ? __builtin_amdgcn_alignbit(hi, lo, sh) : lo) & nm;
+                }
+            }
+        } else {
 #pragma unroll
-        for (int k = 0; k < 16; k++)
-            if (k != 0 && k != 4 && k != 6 && k != 7) PL(P, k, 0) = PL(P, k, 1) = 0u;
+            for (int i = 0; i < 32; i++) P[i] = i < nrows ? gb[((base + i) & (N - 1)) * RS] : 0u;
+            transpose32(P);
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                if (k != 0 && k != 4 && k != 6 && k != 7) PL(P, k, 0) = PL(P, k, 1) = 0u;
+        }
         GeoBand<SPAWN_COUNT> geo{lane, 0, HaloView{0u, 0u}, none, 0, 0, 0, nullptr};
         u32 ch[2];
         rule_planes(P, ch, geo, sc, 0u);
@@ -1137,8 +1186,25 @@ k_env_action_planes128(sl_env_state st, const int32_t *__restrict__ actions, int
         cells = (cells << 16) | (uint64_t)i;
         vals = (vals << 16) | (uint64_t)d;
     }
-    act[st.B + b] = (int64_t)cells;
-    act[2 * st.B + b] = (int64_t)vals;
+    if (st.elig_planes) {
+        // replay: the count prologue (count_env128) puts the edits into the planes and
+        // re-counts the rows round them (act[B + b], as env_action_one leaves them)
+        uint32_t rows = 0xFFFFFFFFu;
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const uint32_t i = (uint32_t)((cells >> (16 * m)) & 0xFFFFu);
+            if (i >= (uint32_t)(N * N)) continue;
+            const uint32_t y = i >> 7;
+            bool seen = false;
+            for (int j = 0; j < 4; j++) seen = seen || ((rows >> (8 * j)) & 0xFFu) == y;
+            if (!seen) rows = (rows << 8) | y;
+        }
+        act[st.B + b] = (int64_t)rows;
+        act[3 * st.B + b] = (int64_t)cells;
+    } else {
+        act[st.B + b] = (int64_t)cells;
+        act[2 * st.B + b] = (int64_t)vals;
+    }
     act[b] = reward;
 }
 
@@ -1199,8 +1265,15 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
     const dim3 grid((unsigned)st.B);
     if (fx.stream) {
         if (stream_counts(fx)) {
-            const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
-            if (rca) return rca;
+            if (fx.plane_mode) {
+                hipLaunchKernelGGL(k_env_action_planes128, dim3((unsigned)((st.B + 255) / 256)),
+                                   dim3(256), 0, s, st, actions, ctp, ctc,
+                                   scratch_of(fx.scratch, st.B).act);
+                if (hipGetLastError() != hipSuccess) return SL_EHIP;
+            } else {
+                const int rca = launch_env_action(st, actions, ctp, ctc, scratch_of(fx.scratch, st.B).act, s);
+                if (rca) return rca;
+            }
             hipLaunchKernelGGL(k_stream_prologue128, grid, dim3(64), 0, s, ka);
             if (hipGetLastError() != hipSuccess) return SL_EHIP;
         }

@@ -1011,7 +1011,9 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     // 128x128 board planes: a Philox step of the fast kernel without views or capture
     // keeps the board in them; any other step first completes (and demotes) it
     const bool planes128 = st->board_planes && st->planes_ok && st->H == 128 && st->W == 128;
-    fx.plane_mode = (fast128 && !replay && planes128 && !cfg->obs_out && !cap) ? 1 : 0;
+    // (replay: with draw planes, the decided form)
+    fx.plane_mode = (fast128 && planes128 && !cfg->obs_out && !cap &&
+                     (!replay || st->elig_planes)) ? 1 : 0;
     if (planes128 && !fx.plane_mode) {
         const int rc = sync_board_planes(*st, 1, s);
         if (rc) return rc;

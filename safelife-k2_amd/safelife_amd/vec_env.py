@@ -188,10 +188,10 @@ class SafeLifeVecEnv:
             s.planes = self.planes.data_ptr()
             s.planes_ok = self.planes_ok.data_ptr()
         self.board_planes = None
-        if (H, W) == (128, 128) and self.rng == "philox":
-            # the 128x128 board in bit planes, kept there by Philox steps without
-            # observations (sl_env_state.board_planes); `board` completes the uint16
-            # tensor when it is read
+        if (H, W) == (128, 128):
+            # the 128x128 board in bit planes, kept there by steps without observations
+            # (sl_env_state.board_planes); `board` completes the uint16 tensor when it
+            # is read
             self.board_planes = z(B, H // 32, 32, 64)
             s.board_planes = self.board_planes.data_ptr()
         if (H, W) == (128, 128) and self.rng == "stream":
