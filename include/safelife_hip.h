@@ -338,7 +338,9 @@ typedef struct sl_env_state {
                                  change): their colours come from the pool's
                                  goal_planes; bit6 (128x128): board_planes hold
                                  the board; bit7: with bit6, the uint16 board
-                                 is complete too (else only its band-edge rows).
+                                 is complete too (else only its band-edge rows);
+                                 bit8: with bit6, the board's planes 12-14 are
+                                 zero and not kept.
                                  Anything
                                  that writes the goals other than the 64x64
                                  kernel and its reset clears it.               */

@@ -441,6 +441,12 @@ k_env_step_bits128(Step128KArgs ka) {
     // only the band-edge rows 32t and 32t + 31 are kept, for the halos
     const bool pmode = (MODE == SPAWN_PHILOX || MODE == SPAWN_DECIDED) && fx.plane_mode;
     const bool pin = pmode && (pok_all & 64);
+    // planes_ok bit 8: the board's planes 12-14 are zero (no cell type uses those bits;
+    // the rule and the actions never set them), so they are neither loaded nor stored.
+    // Decided replay only: in the Philox form the selects cost more than the 6 KiB they
+    // save (70.2 vs 72.9 M env-steps/s, +4 % for replay; profiles/r05am_ab_zero_planes.txt)
+    const bool lo12 = MODE == SPAWN_DECIDED && pin && (pok_all & 256);
+    u32 hi12 = 0u;              // a step into plane mode: any of them set
     const LanePtr<u32> bpl{pmode ? st.board_planes + b * (int64_t)(NB * MW) : nullptr};
     // ... and the cells round the agent the next step's action reads
     // (k_env_action_planes128: row agent_y, column agent_x in rows agent_y +- 1, 2)
@@ -469,7 +475,11 @@ k_env_step_bits128(Step128KArgs ka) {
         u32 pk = 0u;            // plane words the action's edits changed (this lane)
         if (pin) {
 #pragma unroll
-            for (int k = 0; k < 32; k++) P[k] = __builtin_nontemporal_load(&bpl[t * MW + k * 64]);
+            for (int k = 0; k < 32; k++) {
+                const int pl = k & 15;
+                P[k] = (lo12 && pl >= 12 && pl <= 14) ? 0u
+                                                      : __builtin_nontemporal_load(&bpl[t * MW + k * 64]);
+            }
             last = gb[(32 * t + 31) * RS];     // (this band's edge store comes after)
         } else {
             load_pairs_nt<RS>(gb + 32 * t * RS, P);
@@ -646,6 +656,10 @@ k_env_step_bits128(Step128KArgs ka) {
             if (pmode) {        // into plane mode: every plane word, and the rows below
 #pragma unroll
                 for (int k = 0; k < 32; k++) __builtin_nontemporal_store(P[k], &bpl[t * MW + k * 64]);
+                if (MODE == SPAWN_DECIDED) {
+#pragma unroll
+                    for (int w = 0; w < 2; w++) hi12 |= PL(P, 12, w) | PL(P, 13, w) | PL(P, 14, w);
+                }
             }
             if (rb) {
                 // only the changed rows, whole (a wave-uniform branch per row; the 64-byte
@@ -671,7 +685,9 @@ k_env_step_bits128(Step128KArgs ka) {
     // eligible cells (decided replay only: any other step clears it)
     // bit 6: the planes hold the board; bit 7: so does the whole uint16 board (a step
     // into plane mode stored its changed rows as well)
-    const int ok = gok | (me.base ? 8 : 0) | (pmode ? (pin ? 64 : 64 | 128) : 0);
+    const bool z12 = MODE == SPAWN_DECIDED && (pin ? lo12 : __ballot(hi12 != 0u) == 0ull);
+    const int ok = gok | (me.base ? 8 : 0) |
+                   (pmode ? (pin ? 64 : 64 | 128) | (z12 ? 256 : 0) : 0);
     if (ok != pok_all && lane_now() == 0) st.planes_ok[b] = ok;
     // the epilogue's inputs, loaded now (in flight with the row stores) rather than held
     // through the bands: the reward, the bonus term and the record again (L2)
@@ -1240,7 +1256,7 @@ __global__ void __launch_bounds__(64) k_board_sync128(sl_env_state st, int demot
         wait_vm();
         if (ei >= 0) cells[ei] = ev;
     }
-    if (lane == 0) st.planes_ok[b] = demote ? pok & ~(64 | 128) : pok | 128;
+    if (lane == 0) st.planes_ok[b] = demote ? pok & ~(64 | 128 | 256) : pok | 128;
 }
 
 }  // namespace
