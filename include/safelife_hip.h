@@ -64,6 +64,13 @@ extern "C" {
 #define SL_KERNEL_GENERIC 1  /* LDS-staged per-cell kernel, any shape        */
 #define SL_KERNEL_FAST 2     /* require the fast kernel (error if none)      */
 
+/* bits of the replay stream's error flag (scratch word 8B, sl_env_cfg.scratch) */
+#define SL_STREAM_ERR_RANGE 1      /* the supplied stream ran out, or the device
+                                      generator could not serve a step's draw range
+                                      (ring too small, or rewound): re-seed / enlarge */
+#define SL_STREAM_ERR_THRESHOLD 2  /* a bit ring (sl_mt19937.bit_ring) served an env
+                                      whose spawn threshold is not the ring's */
+
 #define SL_MAX_EXITS 8      /* exits tracked per env (benchmark levels have 1) */
 #define SL_BONUS_PERIOD_MAX 16
 
@@ -179,9 +186,10 @@ typedef struct sl_mt19937 {
      * uint32_t, ring_draws / 8 bytes), set iff the draw's double is < bits_thr -- for
      * batches whose envs all spawn with that one threshold (double)(float)p: the
      * replay kernels need only u < p, and the ring then holds 1/64 of the bytes.
-     * rounds must be a multiple of 4 (a block's draws fill whole words).  A step whose
-     * env's threshold differs sets the stream error flag.  bit_ring == 0 (a zeroed
-     * struct): a ring of doubles, bits_thr unused. */
+     * rounds must be a multiple of 4 (a block's draws fill whole words).  A step in
+     * which an env that draws has another threshold sets bit 1 of the stream error
+     * flag (SL_STREAM_ERR_THRESHOLD; bit 0 stays the ring's range error).
+     * bit_ring == 0 (a zeroed struct): a ring of doubles, bits_thr unused. */
     int32_t bit_ring;
     double bits_thr;
 } sl_mt19937;

@@ -39,6 +39,7 @@
 // one 1024-thread block per env).
 #include "sl_bits.h"
 #include "sl_env_action.h"
+#include "sl_obs.h"
 
 using namespace sl;
 using namespace sl::fast;
@@ -277,6 +278,32 @@ __device__ __forceinline__ void next_elig(const u32 pl[8], u32 up, u32 dn, int t
     if (lane == 0) cnt[t] = (uint16_t)n;       // the band's count (<= 4096)
 }
 
+// The goals' colour planes (9-11) of band t: from the rolled pool level's goal planes
+// while the goals are still the level's (gp: two level words and a funnel shift), else
+// from the env's mirror (mg)
+template <class M>
+__device__ __forceinline__ void band_gcol(const u32 *gp, const M &mg, int t, int sdy, int sdx,
+                                          u32 gcol[3][2]) {
+    if (gp) {
+        const int r0 = (32 * t - sdy) & (N - 1), q0 = r0 >> 5, q1 = (q0 + 1) & (NB - 1);
+        const u32 sh = (u32)(r0 & 31);
+        const int c0 = (2 * lane_now() - sdx) & (N - 1), c1 = (c0 + 1) & (N - 1);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const u32 *g0 = gp + (k * NB + q0) * N, *g1 = gp + (k * NB + q1) * N;
+            gcol[k][0] = __builtin_amdgcn_alignbit(g1[c0], g0[c0], sh);
+            gcol[k][1] = __builtin_amdgcn_alignbit(g1[c1], g0[c1], sh);
+        }
+    } else {
+        const u32 *m = mg + t * MW;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            gcol[k][0] = m[(9 + k) * 64];
+            gcol[k][1] = m[(25 + k) * 64];
+        }
+    }
+}
+
 // all kernel arguments in one struct at kernarg offset 0: the epilogue re-reads its
 // pointers where it runs (kargs128()), so they are not held in SGPRs through the bands
 struct Step128KArgs {
@@ -296,14 +323,120 @@ __device__ __forceinline__ const Step128KArgs &kargs128() {
     return *(const Step128KArgs *)kp;
 }
 
+// ---- packed views from the planes (plane mode with obs_out; SafeLifeEnv.get_obs,
+// safelife_env.py:125-155, recenter_view, helper_utils.py:41-74).  A view cell is
+// board + ((goals & COLORS) << 3), white goals removed; the view is centred on the
+// agent with torus wrap.  The board never leaves the planes for it: after band t has
+// advanced and been stored, the band's view-form planes (the goal colour planes added
+// into board planes 12-15 by a bit-sliced 3-bit adder: exact for any board bits) are
+// transposed once and staged as rows in the start-plane spool (free until the next
+// band's DMA), and the view rows that fall in the band are stored from there, lane i
+// taking the flat view cells i, i + 64, ... (coalesced).  A view of at most 96 rows
+// (kViewMaxRows128) meets each band in one run of view rows.  Exits are rewritten after the epilogue
+// (view_exits), where their colour is decided.
+
+__device__ __forceinline__ void view_band(u32 P[32], const u32 gcol[3][2], int t, int agy,
+                                          int agx, __attribute__((address_space(3))) u32 *spool,
+                                          int64_t b) {
+    const Step128KArgs &k = kargs128();
+    const int vh = k.fx.obs_vh, vw = k.fx.obs_vw;
+    const int ty = agy - vh / 2, tx = agx - vw / 2;
+    const int s = (32 * t - ty) & (N - 1);           // view row of the band's row 0
+    int va = 0, vb = 0;
+    if (s < vh) {
+        va = s;
+        vb = min(s + 32, vh);
+    } else if (s + 32 > N) {
+        vb = min(s + 32 - N, vh);
+    }
+    if (va >= vb) return;                            // (wave-uniform)
+    const bool rw = k.fx.obs_rw != 0;
+#pragma unroll
+    for (int w = 0; w < 2; w++) {
+        u32 g0 = gcol[0][w], g1 = gcol[1][w], g2 = gcol[2][w];
+        if (rw) {                                    // white goals are background
+            const u32 wh = g0 & g1 & g2;
+            g0 &= ~wh;
+            g1 &= ~wh;
+            g2 &= ~wh;
+        }
+        const u32 b12 = PL(P, 12, w), b13 = PL(P, 13, w), b14 = PL(P, 14, w);
+        u32 c = b12 & g0;
+        PL(P, 12, w) = b12 ^ g0;
+        const u32 x13 = b13 ^ g1;
+        PL(P, 13, w) = x13 ^ c;
+        c = (b13 & g1) | (c & x13);
+        const u32 x14 = b14 ^ g2;
+        PL(P, 14, w) = x14 ^ c;
+        c = (b14 & g2) | (c & x14);
+        PL(P, 15, w) ^= c;                           // (the carry out of bit 15 drops)
+    }
+    transpose32(P);
+    const int lane = lane_now();
+#pragma unroll
+    for (int y = 0; y < 32; y++) spool[y * 64 + lane] = P[y];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const lds_u16 *cells = (const lds_u16 *)spool;
+    uint16_t *o = k.fx.obs_out + b * (int64_t)(vh * vw);
+    const int i_end = vb * vw, dr = 64 / vw, dc = 64 - dr * vw;
+    int i = va * vw + lane;
+    int r = i / vw, c = i - r * vw;
+#pragma unroll 4
+    for (; i < i_end; i += 64) {
+        const int row = (ty + r - 32 * t) & (N - 1), col = (tx + c) & (N - 1);
+        __builtin_nontemporal_store((uint16_t)cells[row * N + col], &o[i]);
+        r += dr;
+        c += dc;
+        if (c >= vw) {
+            c -= vw;
+            r++;
+        }
+    }
+}
+
+// The exits of the view (recenter_view's move_to_perimeter): every exit cell goes to
+// its clipped position, the last exit in np.nonzero order winning a shared one.  An
+// exit's value is the epilogue's (LEVEL_EXIT, red when the level can be exited: exits
+// are frozen and never change otherwise) plus its goal colour; the goal cell is read
+// past the vector L1 (this wave stored the goals' changed rows).
+__device__ __forceinline__ void view_exits(const sl_env_state &st, int64_t b, int agy, int agx,
+                                           int can) {
+    const Step128KArgs &k = kargs128();
+    const int vh = k.fx.obs_vh, vw = k.fx.obs_vw;
+    const int ne = min(__builtin_amdgcn_readfirstlane(st.exit_count[b]), SL_MAX_EXITS);
+    if (ne <= 0) return;
+    const int lane = lane_now();
+    int tgt = -1;
+    uint16_t val = 0;
+    if (lane < ne) {
+        const int iy = st.exit_y[b * SL_MAX_EXITS + lane], ix = st.exit_x[b * SL_MAX_EXITS + lane];
+        int jy = pymod(iy - agy + N / 2, N) - N / 2;
+        int jx = pymod(ix - agx + N / 2, N) - N / 2;
+        jy = min(max(jy + vh / 2, 0), vh - 1);
+        jx = min(max(jx + vw / 2, 0), vw - 1);
+        tgt = jy * vw + jx;
+        const int ci = iy * N + ix;
+        const u32 *gw = reinterpret_cast<const u32 *>(st.goals + b * (int64_t)(N * N)) + (ci >> 1);
+        const u32 g2 = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u32 ev = LEVEL_EXIT | (can ? COLOR_R : 0u);
+        val = obs::obs_value(ev, (g2 >> (16 * (ci & 1))) & 0xFFFFu, k.fx.obs_rw);
+    }
+    bool last = lane < ne;
+    for (int j = 1; j < ne; j++) {
+        const int tj = __builtin_amdgcn_readlane(tgt, j);
+        if (j > lane && tj == tgt) last = false;
+    }
+    if (last) k.fx.obs_out[b * (int64_t)(vh * vw) + tgt] = val;
+}
+
 // One env-step of env b, after the action: k_env_action has applied it -- state and cell edits in HBM, reward
 // in scratch act[b] -- so this kernel holds no action code, no edit lists and no
 // overlay.  MODE: SPAWN_PHILOX; SPAWN_STREAM (each tensor's first uniform from the
 // scratch offsets); or SPAWN_DECIDED (the spawns from the draw planes k_stream_draw128
 // left, replay with sl_env_state.elig_planes).
-template <int MODE>
-__global__ void __launch_bounds__(64, MODE == SPAWN_STREAM ? kMinWavesStream : kMinWaves)
-k_env_step_bits128(Step128KArgs ka) {
+template <int MODE, bool VIEW>
+__device__ __forceinline__ void step128_body(const Step128KArgs &ka) {
     const sl_env_state &st = ka.st;
     const StepArgs &a = ka.a;
     const FastExtra &fx = ka.fx;
@@ -553,24 +686,7 @@ k_env_step_bits128(Step128KArgs ka) {
         }
         __builtin_amdgcn_sched_barrier(0);
         u32 gcol[3][2];
-        if (gp) {       // the rolled level's band: two level words and a funnel shift
-            const int r0 = (32 * t - sdy) & (N - 1), q0 = r0 >> 5, q1 = (q0 + 1) & (NB - 1);
-            const u32 sh = (u32)(r0 & 31);
-            const int c0 = (2 * lane_now() - sdx) & (N - 1), c1 = (c0 + 1) & (N - 1);
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                const u32 *g0 = gp + (k * NB + q0) * N, *g1 = gp + (k * NB + q1) * N;
-                gcol[k][0] = __builtin_amdgcn_alignbit(g1[c0], g0[c0], sh);
-                gcol[k][1] = __builtin_amdgcn_alignbit(g1[c1], g0[c1], sh);
-            }
-        } else {
-            const u32 *m = mg + t * MW;
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                gcol[k][0] = m[(9 + k) * 64];
-                gcol[k][1] = m[(25 + k) * 64];
-            }
-        }
+        band_gcol(gp, mg, t, sdy, sdx, gcol);
         int p, q, r, e;
         u32 S[32];
         wait_vm();              // the band's start planes have landed in LDS
@@ -580,10 +696,17 @@ k_env_step_bits128(Step128KArgs ka) {
         }
         score_planes(P, gcol, S, &p, &q, &r, &e);
         if (start_hi) e += side_hi_fix(P, gcol, S, gs + 32 * t * RS);
-        pts += p;
-        scr += q;
-        pos += r;
-        side += e;
+        if (VIEW) {     // wave-uniform sums (SGPRs): four VGPRs fewer through the bands
+            pts += wave_total(p);
+            scr += wave_total(q);
+            pos += wave_total(r);
+            side += wave_total(e);
+        } else {
+            pts += p;
+            scr += q;
+            pos += r;
+            side += e;
+        }
         const u32 rb = wave_or(cb[0] | cb[1]);
         if (pin) {
             // the plane words a change can alter: alive, destructible and colours
@@ -669,7 +792,12 @@ k_env_step_bits128(Step128KArgs ka) {
 #pragma unroll
                 for (int y = 0; y < 32; y++)
                     if ((rb >> y) & 1u) __builtin_nontemporal_store(P[y], &gb[(32 * t + y) * RS]);
+                if (VIEW) transpose32(P);        // (a step into plane mode: planes again)
             }
+        }
+        if (VIEW) {             // (the colour words again, from L2: not held through the stores)
+            band_gcol(gp, mg, t, sdy, sdx, gcol);
+            view_band(P, gcol, t, agy, agx, spool, b);
         }
     }
     if (MODE == SPAWN_DECIDED) {
@@ -679,8 +807,9 @@ k_env_step_bits128(Step128KArgs ka) {
         next_elig(EP, r31, pack_row(E0, 0), NB - 1, lane_now(), me, ne_cnt);
         next_elig(E0, pack_row(EP, 31), d1, 0, lane_now(), me, ne_cnt);
     }
-    const int points = wave_total(pts), score = wave_total(scr);
-    const int possible = wave_total(pos), side_total = wave_total(side);
+    const int points = VIEW ? pts : wave_total(pts), score = VIEW ? scr : wave_total(scr);
+    const int possible = VIEW ? pos : wave_total(pos);
+    const int side_total = VIEW ? side : wave_total(side);
     // goals mirror bits, and bit 3 = the board's draw planes hold the advanced board's
     // eligible cells (decided replay only: any other step clears it)
     // bit 6: the planes hold the board; bit 7: so does the whole uint16 board (a step
@@ -700,18 +829,35 @@ k_env_step_bits128(Step128KArgs ka) {
                                              fl.prior_y(fl.prior_head()), fl.prior_len(),
                                              k.a.bonus_period, k.a.bonus_len)];
     wait_vm();              // row stores land before the epilogue rewrites the exits
+    int can = 0;
     if (lane_now() == 0) {
         // (plane mode: the exits' colour is kept in the uint16 cells only -- no rule,
         // score or action term reads an exit's colour, and k_board_sync128 keeps them)
         const bool reset = epilogue_core(k.st, k.a, b, fl, act_reward, points, score, possible,
                                          side_total, k.reward_out, k.done_out, k.flags_out,
-                                         k.ep_len_out, k.ep_rew_out);
+                                         k.ep_len_out, k.ep_rew_out, &can);
         if (k.fx.fuse_reset && reset) {   // queued for k_env_reset_list_wide
             int64_t *cnt = k.fx.scratch + 8 * k.st.B + 2 + (k.a.step & 1);
             const int i = (int)atomicAdd((unsigned long long *)cnt, 1ull);
             reset_list(k.fx.scratch)[i] = (int32_t)b;
         }
     }
+    // (the view's band stores have completed: wait_vm above)
+    if (VIEW) view_exits(k.st, b, agy, agx, __builtin_amdgcn_readfirstlane(can));
+}
+
+// the step kernel: Philox, the stream fallback or decided replay; no views
+template <int MODE>
+__global__ void __launch_bounds__(64, MODE == SPAWN_STREAM ? kMinWavesStream : kMinWaves)
+k_env_step_bits128(Step128KArgs ka) {
+    step128_body<MODE, false>(ka);
+}
+
+// ... with packed views written from the planes (plane mode, fx.obs_out)
+template <int MODE>
+__global__ void __launch_bounds__(64, kMinWaves)
+k_env_step_bits128_view(Step128KArgs ka) {
+    step128_body<MODE, true>(ka);
 }
 
 // Replay-mode count of env b (SL_RNG_STREAM), one wave, after k_env_action (one lane
@@ -1302,7 +1448,10 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
                 hipLaunchKernelGGL(k_stream_draw128, grid, dim3(64), 0, s, ka);
             if (hipGetLastError() != hipSuccess) return SL_EHIP;
             if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-            hipLaunchKernelGGL(k_env_step_bits128<SPAWN_DECIDED>, grid, dim3(64), 0, s, ka);
+            if (fx.plane_mode && fx.obs_out)
+                hipLaunchKernelGGL(k_env_step_bits128_view<SPAWN_DECIDED>, grid, dim3(64), 0, s, ka);
+            else
+                hipLaunchKernelGGL(k_env_step_bits128<SPAWN_DECIDED>, grid, dim3(64), 0, s, ka);
         } else {
             if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
             hipLaunchKernelGGL(k_env_step_bits128<SPAWN_STREAM>, grid, dim3(64), 0, s, ka);
@@ -1318,7 +1467,10 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
             if (rc) return rc;
         }
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        hipLaunchKernelGGL(k_env_step_bits128<SPAWN_PHILOX>, grid, dim3(64), 0, s, ka);
+        if (fx.plane_mode && fx.obs_out)
+            hipLaunchKernelGGL(k_env_step_bits128_view<SPAWN_PHILOX>, grid, dim3(64), 0, s, ka);
+        else
+            hipLaunchKernelGGL(k_env_step_bits128<SPAWN_PHILOX>, grid, dim3(64), 0, s, ka);
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);

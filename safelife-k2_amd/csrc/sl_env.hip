@@ -549,6 +549,20 @@ k_env_reset_list_wide(sl_env_state st, sl_level_pool pool, ResetArgs ra, int64_t
     }
 }
 
+// The packed views of the envs k_env_reset_list_wide reset this step (a 128x128 step
+// whose kernel wrote the other views from the board planes): one wave per listed env,
+// four per workgroup, from the new episode's uint16 board (written by the previous
+// launch).
+__global__ void __launch_bounds__(256)
+k_env_obs_reset_list(sl_env_state st, ObsArgs a, const int64_t *scratch, uint32_t step,
+                     uint16_t *out) {
+    const int n = (int)scratch[8 * st.B + 2 + (step & 1)];
+    const int32_t *list = reset_list(const_cast<int64_t *>(scratch));
+    const int lane = threadIdx.x & 63;
+    for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4)
+        obs_packed_wave(st, a, list[i], lane, out);
+}
+
 // pool->board_planes (H == 64): [k][p][x] bit y = bit p of pool->board[k][y][x];
 // (H == 128): 32-bit words [k][p][q][x] bit r = bit p of pool->board[k][32q + r][x]
 __global__ void __launch_bounds__(NT) k_pool_planes(sl_level_pool pool) {
@@ -802,6 +816,13 @@ int launch_env_action(const sl_env_state &st, const int32_t *actions, int ctp, i
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
+int launch_obs_reset_list(const sl_env_state &st, const ObsArgs &a, uint16_t *out,
+                          const int64_t *scratch, uint32_t step, hipStream_t s) {
+    const unsigned grid = (unsigned)(st.B < 1024 ? (st.B + 3) / 4 : 256);
+    hipLaunchKernelGGL(k_env_obs_reset_list, dim3(grid), dim3(256), 0, s, st, a, scratch, step, out);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
 int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
                            int64_t *scratch, uint32_t step, hipStream_t s) {
     const unsigned grid = (unsigned)(st.B < 256 ? st.B : 256);
@@ -888,13 +909,14 @@ extern "C" int sl_level_pool_prepare(sl_level_pool *pool, void *stream) {
 
 namespace {
 // A bit ring serves only envs whose threshold is the ring's: any env that draws this
-// step with another one flags the stream error (its spawns would be wrong).
+// step with another one flags the stream error -- bit 1 (SL_STREAM_ERR_THRESHOLD), not
+// the ring's range bit 0: the fix is a ring of doubles, not a re-seed
 __global__ void __launch_bounds__(256)
 k_bits_thr_check(const float *__restrict__ spawn_prob, const int64_t *__restrict__ counts,
                  int64_t B, double thr, int64_t *__restrict__ err) {
     const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (b < B && (counts[2 * b] | counts[2 * b + 1]) && (double)spawn_prob[b] != thr)
-        atomicOr((unsigned long long *)err, 1ull);
+        atomicOr((unsigned long long *)err, (unsigned long long)SL_STREAM_ERR_THRESHOLD);
 }
 }  // namespace
 
@@ -1008,23 +1030,27 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     // their reset-list kernel, so they keep the list (and its per-parity lengths,
     // which only the reset-list kernel clears) going through captured steps.
     if (cap && small) fx.fuse_reset = 0;
-    // 128x128 board planes: a Philox step of the fast kernel without views or capture
-    // keeps the board in them; any other step first completes (and demotes) it
-    const bool planes128 = st->board_planes && st->planes_ok && st->H == 128 && st->W == 128;
-    // (replay: with draw planes, the decided form)
-    fx.plane_mode = (fast128 && planes128 && !cfg->obs_out && !cap &&
-                     (!replay || st->elig_planes)) ? 1 : 0;
-    if (planes128 && !fx.plane_mode) {
-        const int rc = sync_board_planes(*st, 1, s);
-        if (rc) return rc;
-    }
-    // observations: packed views of 64x64 boards come out of the step kernel itself
     ObsArgs oa;
     if (cfg->obs_out) {
         const int rc = obs_args(cfg->obs_vh, cfg->obs_vw, cfg->obs_remove_white, cfg->obs_mode,
                                 cfg->obs_channels, cfg->obs_nch, &oa);
         if (rc) return rc;
     }
+    // 128x128 board planes: a step of the fast kernel without capture keeps the board
+    // in them -- with no views, or with packed views of at most kViewMaxRows rows,
+    // which the step kernel writes from the planes (fuse_obs128); any other step first
+    // completes (and demotes) it.  (Replay: with draw planes, the decided form.)
+    const bool planes128 = st->board_planes && st->planes_ok && st->H == 128 && st->W == 128;
+    const bool fuse_obs128 = fast128 && planes128 && cfg->obs_out && !cap &&
+                             (!replay || st->elig_planes) && oa.mode == SL_OBS_PACKED &&
+                             oa.vh <= kViewMaxRows128 && oa.vw <= 128;
+    fx.plane_mode = (fast128 && planes128 && (!cfg->obs_out || fuse_obs128) && !cap &&
+                     (!replay || st->elig_planes)) ? 1 : 0;
+    if (planes128 && !fx.plane_mode) {
+        const int rc = sync_board_planes(*st, 1, s);
+        if (rc) return rc;
+    }
+    // observations: packed views of 64x64 boards come out of the step kernel itself
     // ... and channel views too (one wave writes its env's 16-byte chunks from the
     // view masks it builds in LDS: views up to kFusedChanCells cells, 16-B aligned out)
     const bool fuse_obs =
@@ -1032,7 +1058,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         ((oa.mode == SL_OBS_PACKED && oa.vh * oa.vw <= kObsMaxCells) ||
          (oa.mode != SL_OBS_PACKED && oa.vh <= 64 && oa.vw <= 64 &&
           oa.vh * oa.vw + 2 <= kFusedChanCells && (((uintptr_t)cfg->obs_out) & 15) == 0));
-    fx.obs_out = fuse_obs ? (uint16_t *)cfg->obs_out : nullptr;
+    fx.obs_out = (fuse_obs || fuse_obs128) ? (uint16_t *)cfg->obs_out : nullptr;
     fx.obs_vh = cfg->obs_vh;
     fx.obs_vw = cfg->obs_vw;
     fx.obs_rw = cfg->obs_remove_white;
@@ -1107,7 +1133,15 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         if (hipGetLastError() != hipSuccess) return SL_EHIP;
     }
     if (cfg->obs_out) {
-        if (!fuse_obs || (cfg->auto_reset && !reset_done)) {
+        if (fuse_obs128) {
+            // the step kernel wrote every view from the planes; the envs the reset-list
+            // kernel reset get theirs from the new episode's uint16 board
+            if (reset_done) {
+                const int rc = launch_obs_reset_list(*st, oa, (uint16_t *)cfg->obs_out,
+                                                     cfg->scratch, cfg->step, s);
+                if (rc) return rc;
+            }
+        } else if (!fuse_obs || (cfg->auto_reset && !reset_done)) {
             const int rc = launch_obs(*st, oa, cfg->obs_out, s);
             if (rc) return rc;
         }

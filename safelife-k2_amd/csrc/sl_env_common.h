@@ -347,8 +347,10 @@ struct FastExtra {
     const int64_t *stream_base;   // *stream_base + the step
     const sl_mt19937 *mt;   // replay from the device generator (sl_env_cfg.mt) or NULL:
                             // stream_offsets fills its ring for the step's range
-    int32_t plane_mode = 0; // 128x128 Philox without views or capture, board_planes set:
-                            // the board is kept in sl_env_state.board_planes
+    int32_t plane_mode = 0; // 128x128 step without capture (no views, or packed views of
+                            // <= kViewMaxRows128 rows written from the planes; replay
+                            // with draw planes), board_planes set: the board is kept in
+                            // sl_env_state.board_planes
 };
 // replay-mode phases of a bit-sliced launcher: whether it runs the action + count
 // prologue, and whether it continues past the offsets scan to the step kernel
@@ -390,6 +392,9 @@ int launch_env_action(const sl_env_state &st, const int32_t *actions, int ctp, i
 // block each (sl_env.hip)
 int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, const ResetArgs &ra,
                            int64_t *scratch, uint32_t step, hipStream_t s);
+// the 128x128 step kernel writes packed views of at most this many rows from the board
+// planes (sl_bits128.hip view_band: one run of view rows per 32-row band)
+constexpr int kViewMaxRows128 = 96;
 // bit-sliced 64x64 kernel (sl_bits.hip)
 int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,

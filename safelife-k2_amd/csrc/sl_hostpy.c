@@ -7,8 +7,9 @@
  *     board: the caller's object; spawn_prob: a float (converted to C float, as the
  *     reference's "f" format does); draws: float64 [n], the 10 000-double spawn
  *     buffer; pos: int64 [1], the buffer position, advanced by the draws consumed.
- *     None: draws[pos:] is too short for this board (nothing consumed; the caller
- *     refills as the reference does and calls advance_with).  NotImplemented: board is
+ *     None: draws[pos:] (possibly empty) is too short for this board (nothing
+ *     consumed; the caller takes the board's draws as the reference does, refilling
+ *     only when one is needed, and calls advance_with).  NotImplemented: board is
  *     not a C-contiguous uint16 2-d ndarray with 2 <= H and 2 <= W <= 512 (the caller
  *     converts or validates it).
  *   advance_with(board, spawn_prob, draws) -> new board: exactly len(draws) uniforms
@@ -61,7 +62,9 @@ static PyObject *py_advance(PyObject *self, PyObject *const *args, Py_ssize_t na
     }
     int64_t *pos = (int64_t *)PyArray_DATA((PyArrayObject *)po);
     const int64_t nd = PyArray_SIZE(d);
-    if (*pos < 0 || *pos >= nd) Py_RETURN_NONE;
+    /* a used-up buffer (pos == nd) still serves a board that needs no draw: the
+     * reference refills only when a draw is taken (random.c:47-52) */
+    if (*pos < 0 || *pos > nd) Py_RETURN_NONE;
     PyArrayObject *b = (PyArrayObject *)args[0];
     PyArrayObject *out = (PyArrayObject *)PyArray_NewLikeArray(b, NPY_CORDER, NULL, 0);
     if (!out) return NULL;

@@ -15,6 +15,7 @@ CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 SL_OK, SL_EINVAL, SL_EHIP, SL_ETOOBIG = 0, -1, -2, -3
 SL_RNG_STREAM, SL_RNG_PHILOX = 0, 1
 SL_KERNEL_AUTO, SL_KERNEL_GENERIC, SL_KERNEL_FAST = 0, 1, 2
+SL_STREAM_ERR_RANGE, SL_STREAM_ERR_THRESHOLD = 1, 2
 SL_MAX_EXITS = 8
 SL_BONUS_PERIOD_MAX = 16
 SL_OBS_NONE, SL_OBS_PACKED, SL_OBS_CHANNELS, SL_OBS_CHANNELS_U8 = 0, 1, 2, 3

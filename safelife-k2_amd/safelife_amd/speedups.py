@@ -168,13 +168,13 @@ def advance_board(board, spawn_prob=0.3):
         raise ValueError("advance_board needs H, W >= 2")
     if W > 512:
         return _advance_device_numpy(a, float(np.float32(spawn_prob)))
-    if b.pos >= _RAND_BUFFER_SIZE:
-        b.refill()
     r = _host().advance(a, spawn_prob, b.buf, b.posarr)
     if r is not None:
         return r
     # the board needs more uniforms than the buffer still holds: take them as the
-    # reference does (refilled from the global stream when the buffer runs out)
+    # reference does, refilling from the global stream only when a draw is taken and
+    # the buffer is used up (random.c:47-52) -- a board with no eligible cell never
+    # refills, so np.random calls after it see the reference's global state
     return _host().advance_with(a, spawn_prob, b.take(_host().count_eligible(a)))
 
 

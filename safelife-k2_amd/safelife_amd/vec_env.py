@@ -158,7 +158,6 @@ class SafeLifeVecEnv:
         torch, dev, B, H, W = self.torch, self.device, self.B, self.H, self.W
         z = lambda *s, dt=torch.int32: torch.zeros(s, dtype=dt, device=dev)
         self._board = z(B, H, W, dt=torch.uint16)
-        self._board_stale = False
         self.goals = z(B, H, W, dt=torch.uint16)
         self.start_board = z(B, H, W, dt=torch.uint16)
         self.st_t = {
@@ -246,7 +245,6 @@ class SafeLifeVecEnv:
         # running episodes' start boards are no longer levels of the pool: the
         # kernels read them from HBM until those envs are reset from the new pool
         self.st_t["start_roll"].fill_(-1)
-        self._board_stale = False      # (planes_ok is zeroed: the uint16 board holds)
 
     # ------------------------------------------------- the device generator's ring
     @staticmethod
@@ -493,8 +491,6 @@ class SafeLifeVecEnv:
             cfg.stream_phase = 2
             cfg.stream_base = self._stream_base.data_ptr()
         launch()
-        if self.board_planes is not None:
-            self._board_stale = True
         self._step_index += 1
         self.global_counter.num_steps += self.B
         if self.mt is not None and self._step_index % self.STREAM_CHECK_EVERY == 0:
@@ -513,13 +509,24 @@ class SafeLifeVecEnv:
         if getattr(self, "_err_h", None) is None:
             self._err_h = torch.zeros(1, dtype=torch.int64, pin_memory=True)
             self._err_ev = None
-        if self._err_ev is not None and self._err_ev.query() and int(self._err_h[0]) & 1:
-            raise RuntimeError("rng='stream': the device generator could not serve a step's "
-                               "draw range (ring too small for the draws per step, or a "
-                               "rewind); re-seed with seek_stream / a larger ring")
+        if self._err_ev is not None and self._err_ev.query():
+            self._raise_stream_error(int(self._err_h[0]))
         self._err_h.copy_(self.scratch[8 * self.B:8 * self.B + 1], non_blocking=True)
         self._err_ev = torch.cuda.Event()
         self._err_ev.record(torch.cuda.current_stream(self.device))
+
+    @staticmethod
+    def _raise_stream_error(flag):
+        if flag & _lib.SL_STREAM_ERR_THRESHOLD:
+            raise RuntimeError("rng='stream': an env drew with a spawn threshold other than "
+                               "the device generator's bit ring holds (spawn_prob changed "
+                               "outside set_state / load_state_dict / set_pool, e.g. by "
+                               "writing st_t['spawn_prob'] directly); rebuild the ring with "
+                               "stream_ring='doubles' or through set_state")
+        if flag & _lib.SL_STREAM_ERR_RANGE:
+            raise RuntimeError("rng='stream': the device generator could not serve a step's "
+                               "draw range (ring too small for the draws per step, or a "
+                               "rewind); re-seed with seek_stream / a larger ring")
 
     # ------------------------------------------------- the reference's PPO loop order
     def step_env_reference(self, e, action, *, reward_out=None, done_out=None, obs_out=None,
@@ -606,7 +613,7 @@ class SafeLifeVecEnv:
 
     @staticmethod
     def stream_error_of(scratch, B):
-        return bool(scratch[8 * B].item() & 1)
+        return bool(scratch[8 * B].item() & (_lib.SL_STREAM_ERR_RANGE | _lib.SL_STREAM_ERR_THRESHOLD))
 
     def _check_reset_lists(self):
         """Zero the per-parity reset-list lengths (scratch[8B+2 : 8B+4]) unless this
@@ -680,18 +687,19 @@ class SafeLifeVecEnv:
 
     @property
     def board(self):
-        """uint16 [B, H, W] boards.  A 128x128 batch stepped without observations keeps
-        its boards in bit planes (sl_env_state.board_planes); reading this completes
-        the tensor first (sl_env_board_sync, stream-ordered).  Write boards through
-        set_state / load_state_dict (or clear planes_ok after writing)."""
-        if self._board_stale:
-            self.sync_board()
+        """uint16 [B, H, W] boards.  A 128x128 batch keeps its boards in bit planes
+        across its steps (sl_env_state.board_planes); reading this always completes the
+        tensor first (sl_env_board_sync, stream-ordered).  Whether an env's uint16 board
+        is complete is decided on the device, per env (planes_ok bits 6-7), never by a
+        host flag: an env whose board is already complete costs its workgroup one load.
+        Write boards through set_state / load_state_dict (or clear planes_ok after
+        writing)."""
+        self.sync_board()
         return self._board
 
     def sync_board(self):
         """Complete the uint16 boards of envs whose board lives in planes (no-op
         otherwise; no host sync)."""
-        self._board_stale = False
         L = _lib.lib()
         # (an A/B build of an older revision, SAFELIFE_HIP_LIB, has no board planes)
         if self.board_planes is not None and hasattr(L, "sl_env_board_sync"):
@@ -707,7 +715,8 @@ class SafeLifeVecEnv:
     def stream_error(self):
         """True if rng='stream' ran past the end of the supplied stream (or asked the
         device generator for a range it could not serve)."""
-        return bool(self.scratch[8 * self.B].item() & 1)
+        return bool(self.scratch[8 * self.B].item()
+                    & (_lib.SL_STREAM_ERR_RANGE | _lib.SL_STREAM_ERR_THRESHOLD))
 
     def set_state(self, board, goals, start_board, **scalars):
         """Load explicit state (for tests / checkpoints).  Arrays are [B,...]."""
@@ -724,7 +733,6 @@ class SafeLifeVecEnv:
         longer match pool levels (kernels read them from HBM), the bit-plane
         mirrors are stale and the reset lists start empty."""
         self.st_t["start_roll"].fill_(-1)
-        self._board_stale = False      # (planes_ok is zeroed: the uint16 board holds)
         # may hold spawners (replay counts them); bit 2 (128x128 boards): the start board
         # uses cell bits 12-14, which the 128x128 kernel then compares in a second pass
         hi = start_board_hi_bits(self.start_board) & ((self.H, self.W) == (128, 128))

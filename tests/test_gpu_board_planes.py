@@ -147,5 +147,85 @@ def test_game_entries_complete_the_board(torch_dev):
     _lib.check(L.sl_env_rescore(ctypes.byref(b._state), pb.data_ptr(), _lib.stream_ptr(dev)),
                "sl_env_rescore")
     assert torch.equal(pa, pb)
-    a._board_stale = False               # (the entry completed it)
-    assert torch.equal(a._board, b.board)
+    assert torch.equal(a._board, b.board)   # (the entry completed it, before any read)
+
+
+def test_plane_mode_across_pool_swaps_and_state_dict(torch_dev):
+    """set_pool / PoolFeeder.swap between plane steps, then
+    venv.board and state_dict() read straight after the swap (before any step), must
+    be the uint16-only form's; a checkpoint taken there restores it, and both run on
+    identically for 20 more steps (file_finder.py:143-201 is the reference's reset
+    source; safelife_env.py:177-185 the board a caller sees after each step)."""
+    torch, dev = torch_dev
+    from safelife_amd import LevelPool
+    from safelife_amd.pool_feed import PoolFeeder, npz_level_source
+    B = 256
+    a, b = _pair(torch_dev, B, seed=21, tl=15)
+    full = LevelPool.load(C5)
+    order2, order3 = [2, 3, 0, 1], [3, 1, 0, 2]
+    lv = list(npz_level_source(C5, repeat=False))
+    feeder = PoolFeeder((lv[i] for i in order2), pool_size=4, device=dev)
+    rng = np.random.RandomState(13)
+    try:
+        for t in range(62):
+            if t == 20:                # the feeder's swap vs a synchronous set_pool
+                assert feeder.swap(a, block=True, timeout=60)
+                b.set_pool(full.subset(order2))
+                assert ((a.planes_ok & 64) != 0).any()      # boards in planes
+                _same_state(a, b, "after swap")
+            if t == 41:                # state_dict first, with no board read before it
+                a.set_pool(full.subset(order3))
+                b.set_pool(full.subset(order3))
+                assert ((a.planes_ok & 64) != 0).any()
+                da, db = a.state_dict(), b.state_dict()
+                for k in db:
+                    if k != "step_index":
+                        assert torch.equal(da[k], db[k]), k
+                a.load_state_dict(da)
+                b.load_state_dict(db)
+            acts = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+            a.step_async(acts)
+            b.step_async(acts)
+            for x, y in ((a.reward, b.reward), (a.done, b.done), (a.flags, b.flags)):
+                assert torch.equal(x, y), t
+        assert feeder.swaps == 1
+        _same_state(a, b, "end")
+    finally:
+        feeder.close()
+
+
+@pytest.mark.parametrize("view,rw", [((33, 33), True), ((15, 15), False), ((96, 40), True),
+                                     ((1, 128), True), ((97, 33), True), ((34, 7), False)])
+def test_plane_mode_views_match_uint16_views(torch_dev, view, rw):
+    """Packed views written by the 128x128 step kernel from the board planes (round 6:
+    views of at most 96 rows keep the batch in plane mode; get_obs,
+    safelife_env.py:125-155, recenter_view, helper_utils.py:41-74) equal those of the
+    uint16-only form, every step, through resets (the reset envs' views come from the
+    reset list's obs kernel) and exits moved to the view's edge; a 97-row view takes
+    the unfused path.  Boards and scalars stay equal too."""
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    torch, dev = torch_dev
+    B, T = 384, 40
+    kw = dict(time_limit=11, view_shape=view, penalty_coef=1.0, min_performance=0.01,
+              rng="philox", seed=5, level_order="random", augment_roll=True, kernel="fast",
+              output_channels=None, remove_white_goals=rw)
+    a = SafeLifeVecEnv(LevelPool.load(C5), B, dev, **kw)
+    b = SafeLifeVecEnv(LevelPool.load(C5), B, dev, **kw)
+    b._state.board_planes = None
+    b.board_planes = None
+    oa, ob = a.reset(), b.reset()
+    assert torch.equal(oa, ob)
+    rng = np.random.RandomState(8)
+    fused = view[0] <= 96
+    for t in range(T):
+        acts = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+        oa, ra, da, _ = a.step(acts)
+        ob, rb, db, _ = b.step(acts)
+        assert torch.equal(ra, rb) and torch.equal(da, db), t
+        assert torch.equal(oa, ob), (t, int((oa != ob).flatten(1).any(1).sum()))
+        if t == 20:
+            _same_state(a, b, t)
+        if t >= 2:      # the boards stay in planes when the view is fused
+            inp = int(((a.planes_ok & 64) != 0).sum().item())
+            assert (inp > B // 2) if fused else inp == 0, (t, inp)
+    _same_state(a, b, "end")

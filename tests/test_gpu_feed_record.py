@@ -20,17 +20,21 @@ def torch_dev():
 
 
 # ------------------------------------------------------------------ pool feeder
-@pytest.mark.parametrize("pool_name", ["c3_prune_still_64", "c2_append_still_25"])
+@pytest.mark.parametrize("pool_name", ["c3_prune_still_64", "c2_append_still_25",
+                                       "c5_navigation_128"])
 def test_pool_feeder_swap_matches_set_pool(torch_dev, pool_name):
     """Levels produced on a host thread, uploaded on a side stream and swapped in
     between steps give exactly the run of a synchronous set_pool at the same step;
-    resets after the swap draw from the new levels."""
+    resets after the swap draw from the new levels.  At 128x128 the boards live in
+    bit planes between the reads (test_gpu_board_planes.py checks that form against
+    the uint16-only one across swaps)."""
     torch, dev = torch_dev
     from safelife_amd import SafeLifeVecEnv, LevelPool
     from safelife_amd.pool_feed import PoolFeeder, npz_level_source
     path = os.path.join(POOLS, pool_name + ".npz")
     full = LevelPool.load(path)
-    first, second = full.subset(range(0, 8)), full.subset(range(8, 24))
+    n1, n2 = (8, 24) if full.K >= 24 else (2, 4)
+    first, second = full.subset(range(0, n1)), full.subset(range(n1, n2))
     B, T, swap_at = 64, 90, 30
     kw = dict(time_limit=20, view_shape=(9, 9), output_channels=None, penalty_coef=1.0,
               min_performance=0.01, rng="philox", seed=4, kernel="auto")
@@ -38,8 +42,8 @@ def test_pool_feeder_swap_matches_set_pool(torch_dev, pool_name):
     b = SafeLifeVecEnv(first, B, dev, **kw)
     a.reset()
     b.reset()
-    src = (lv for lv in list(npz_level_source(path, repeat=False))[8:24])
-    feeder = PoolFeeder(src, pool_size=16, device=dev)
+    src = (lv for lv in list(npz_level_source(path, repeat=False))[n1:n2])
+    feeder = PoolFeeder(src, pool_size=n2 - n1, device=dev)
     g = torch.Generator(device=dev)
     g.manual_seed(1)
     try:

@@ -130,6 +130,43 @@ def test_buffer_refill_inside_one_board():
     assert speedups._buffer.pos == ref.pos
 
 
+def test_used_up_buffer_refills_only_when_a_draw_is_taken():
+    """random.c:47-52 refills inside random_float, i.e. only when a draw is taken: a
+    board with no eligible cell leaves a used-up buffer (and numpy's global stream)
+    alone -- the first call of a process included, where the buffer starts used up
+    (buffer_pos = RAND_BUFFER_SIZE, random.c:12).  Later np.random calls (proc_gen.py's,
+    which share the global stream) must see the reference's state."""
+    rng = np.random.RandomState(3)
+    still = np.zeros((20, 30), np.uint16)
+    still[5:7, 5:7] = 1                         # a block: alive, no spawner
+    assert oracle.count_eligible(still) == 0
+    soup = _spawner_soup(rng, 20, 30)
+    n = oracle.count_eligible(soup)
+    assert n > 0
+    for start in ("fresh", "seeded"):
+        np.random.seed(11)
+        if start == "fresh":                    # a process's first call: buffer used up
+            speedups._buffer.pos = 10000
+        else:
+            speedups.seed(11)                   # reseeds and refills: 10 000 drawn
+            speedups._buffer.take(10000)        # used up again
+        drawn = 0 if start == "fresh" else 10000
+        for _ in range(3):
+            assert np.array_equal(speedups.advance_board(still, 0.3), oracle.advance(
+                still, 0.3, draws=np.zeros(0), pos=0)[0])
+        assert speedups._buffer.pos == 10000    # nothing taken, nothing refilled
+        probe = np.random.get_state()
+        # the global stream was not touched: its next value is draw `drawn` of seed 11
+        assert np.random.random() == np.random.RandomState(11).random_sample(drawn + 1)[-1]
+        np.random.set_state(probe)
+        # a board that draws refills now, from the global stream where it stands
+        got = speedups.advance_board(soup, 0.3)
+        ref_buf = np.random.RandomState(11).random_sample(drawn + 10000)[drawn:]
+        want, _ = oracle.advance(soup, 0.3, draws=ref_buf[:n], pos=0)
+        assert np.array_equal(got, want), start
+        assert speedups._buffer.pos == n
+
+
 def test_input_conversion_and_errors():
     rng = np.random.RandomState(1)
     b = _spawner_soup(rng, 20, 30)
