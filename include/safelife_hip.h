@@ -71,6 +71,14 @@ extern "C" {
 #define SL_STREAM_ERR_THRESHOLD 2  /* a bit ring (sl_mt19937.bit_ring) served an env
                                       whose spawn threshold is not the ring's */
 
+/* sl_env_cfg.board_mode: a 128x128 step without capture -- with no views, or with
+ * packed views of at most 96 rows -- keeps the board in sl_env_state.board_planes
+ * (SL_BOARD_AUTO) and writes only a few uint16 rows; a caller that reads the uint16
+ * board after (nearly) every step asks for it whole instead (SL_BOARD_UINT16: the step
+ * kernel writes every changed row, and no sync is needed before a read) */
+#define SL_BOARD_AUTO 0
+#define SL_BOARD_UINT16 1
+
 #define SL_MAX_EXITS 8      /* exits tracked per env (benchmark levels have 1) */
 #define SL_BONUS_PERIOD_MAX 16
 
@@ -366,17 +374,22 @@ typedef struct sl_env_state {
     uint32_t *board_planes;   /* 128x128, or NULL: [B,4,32,64] u32 in the goals
                                  mirror's layout ([b][t][q][lane], word q =
                                  plane q & 15 of column 2 lane + (q >> 4), rows
-                                 32t..32t+31).  When set, a Philox step of the
-                                 fast kernel without obs_out or capture keeps
+                                 32t..32t+31).  When set, a step of the fast
+                                 kernel without capture -- Philox or replay with
+                                 draw planes; no obs_out, or packed views of at
+                                 most 96 rows, which it writes from the planes;
+                                 sl_env_cfg.board_mode SL_BOARD_AUTO -- keeps
                                  the board here (planes_ok bit6) and writes of
                                  the uint16 board only its band-edge rows (32t,
                                  32t + 31) and the cells the action and exits
                                  edit: bit7 then says the uint16 board is
-                                 complete.  sl_env_board_sync completes it; the
-                                 library's other entry points that read or
-                                 write st->board do so themselves.  A caller
-                                 that writes the uint16 board clears planes_ok
-                                 (as for the goals mirror).                    */
+                                 complete.  sl_env_board_sync completes it (a
+                                 per-env no-op for envs not in planes or
+                                 already complete); the library's other entry
+                                 points that read or write st->board do so
+                                 themselves.  A caller that writes the uint16
+                                 board clears planes_ok (as for the goals
+                                 mirror).                                      */
 } sl_env_state;
 
 /* A device-resident level pool (the level_iterator's levels). */
@@ -495,6 +508,8 @@ typedef struct sl_env_cfg {
                                        fills it for the step's range, so the
                                        stream is RandomState(seed) from
                                        *stream_pos on with no host buffer      */
+    int32_t board_mode;             /* SL_BOARD_*: where a 128x128 step leaves the
+                                       board (sl_env_state.board_planes)       */
 } sl_env_cfg;
 
 /*

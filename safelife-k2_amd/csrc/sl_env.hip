@@ -1041,11 +1041,13 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     // which the step kernel writes from the planes (fuse_obs128); any other step first
     // completes (and demotes) it.  (Replay: with draw planes, the decided form.)
     const bool planes128 = st->board_planes && st->planes_ok && st->H == 128 && st->W == 128;
+    if (cfg->board_mode != SL_BOARD_AUTO && cfg->board_mode != SL_BOARD_UINT16) return SL_EINVAL;
     const bool fuse_obs128 = fast128 && planes128 && cfg->obs_out && !cap &&
+                             cfg->board_mode != SL_BOARD_UINT16 &&
                              (!replay || st->elig_planes) && oa.mode == SL_OBS_PACKED &&
                              oa.vh <= kViewMaxRows128 && oa.vw <= 128;
     fx.plane_mode = (fast128 && planes128 && (!cfg->obs_out || fuse_obs128) && !cap &&
-                     (!replay || st->elig_planes)) ? 1 : 0;
+                     (!replay || st->elig_planes) && cfg->board_mode != SL_BOARD_UINT16) ? 1 : 0;
     if (planes128 && !fx.plane_mode) {
         const int rc = sync_board_planes(*st, 1, s);
         if (rc) return rc;

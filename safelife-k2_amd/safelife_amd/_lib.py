@@ -16,6 +16,7 @@ SL_OK, SL_EINVAL, SL_EHIP, SL_ETOOBIG = 0, -1, -2, -3
 SL_RNG_STREAM, SL_RNG_PHILOX = 0, 1
 SL_KERNEL_AUTO, SL_KERNEL_GENERIC, SL_KERNEL_FAST = 0, 1, 2
 SL_STREAM_ERR_RANGE, SL_STREAM_ERR_THRESHOLD = 1, 2
+SL_BOARD_AUTO, SL_BOARD_UINT16 = 0, 1
 SL_MAX_EXITS = 8
 SL_BONUS_PERIOD_MAX = 16
 SL_OBS_NONE, SL_OBS_PACKED, SL_OBS_CHANNELS, SL_OBS_CHANNELS_U8 = 0, 1, 2, 3
@@ -65,7 +66,8 @@ class EnvCfg(ctypes.Structure):
                 ("ev_begin", vp), ("ev_end", vp), ("kernel", i32),
                 ("obs_out", vp), ("obs_mode", i32), ("obs_vh", i32), ("obs_vw", i32),
                 ("obs_remove_white", i32), ("obs_nch", i32), ("obs_channels", i32 * 16),
-                ("capture", vp), ("stream_phase", i32), ("stream_base", vp), ("mt", vp)]
+                ("capture", vp), ("stream_phase", i32), ("stream_base", vp), ("mt", vp),
+                ("board_mode", i32)]
 
 
 class MT19937(ctypes.Structure):

@@ -74,7 +74,7 @@ class SafeLifeVecEnv:
                  level_order="sequential", augment_roll=False, env0=0, n_total_envs=None,
                  can_toggle_powers=False, can_toggle_colors=False, obs_dtype="uint16",
                  compute_obs=True, global_counter=None, kernel="auto", stream_exchange=None,
-                 stream_ring="auto"):
+                 stream_ring="auto", board_mode="auto"):
         import torch
         self.torch = torch
         self.device = _lib.require_device(device)
@@ -113,6 +113,16 @@ class SafeLifeVecEnv:
         if stream_ring not in ("auto", "doubles"):
             raise ValueError("stream_ring must be 'auto' or 'doubles'")
         self.stream_ring = stream_ring
+        # where a 128x128 step leaves the board (sl_env_cfg.board_mode): "planes" keeps
+        # it in bit planes whenever the kernel can (a `board` read then completes the
+        # uint16 tensor first); "uint16" has every step write the changed rows; "auto"
+        # is "planes" unless `board` was read within the last BOARD_READ_WINDOW steps --
+        # a caller reading the board after every step (info['board'],
+        # safelife_env.py:177-178) gets the kernel that writes it, not a sync per read
+        if board_mode not in ("auto", "planes", "uint16"):
+            raise ValueError("board_mode must be 'auto', 'planes' or 'uint16'")
+        self.board_mode = board_mode
+        self._board_read_at = None   # step index of the last `board` read
         self._step_index = 0
         # step index and auto_reset flag of the last launched step: the 64x64 and
         # 128x128 kernels queue finished envs in per-parity lists (sl_env_cfg.scratch)
@@ -371,7 +381,16 @@ class SafeLifeVecEnv:
         c.n_total_envs = self.n_total_envs
         c.augment_roll = int(self.augment_roll)
         c.kernel = self.kernel
+        c.board_mode = _lib.SL_BOARD_UINT16 if self._wants_uint16_board() else _lib.SL_BOARD_AUTO
         return c
+
+    BOARD_READ_WINDOW = 4
+
+    def _wants_uint16_board(self):
+        if self.board_mode != "auto":
+            return self.board_mode == "uint16"
+        return (self._board_read_at is not None
+                and self._step_index - self._board_read_at <= self.BOARD_READ_WINDOW)
 
     # -------------------------------------------------------------- gym-ish API
     def reset(self, mask=None):
@@ -693,7 +712,9 @@ class SafeLifeVecEnv:
         is complete is decided on the device, per env (planes_ok bits 6-7), never by a
         host flag: an env whose board is already complete costs its workgroup one load.
         Write boards through set_state / load_state_dict (or clear planes_ok after
-        writing)."""
+        writing).  With board_mode="auto" a read also makes the next
+        BOARD_READ_WINDOW steps write the uint16 board themselves."""
+        self._board_read_at = self._step_index
         self.sync_board()
         return self._board
 

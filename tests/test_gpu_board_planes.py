@@ -33,7 +33,7 @@ def _pair(torch_dev, B, seed, tl):
     torch, dev = torch_dev
     kw = dict(time_limit=tl, view_shape=(33, 33), penalty_coef=1.0, min_performance=0.01,
               rng="philox", seed=seed, level_order="random", augment_roll=True,
-              kernel="fast", compute_obs=False)
+              kernel="fast", compute_obs=False, board_mode="planes")
     a = SafeLifeVecEnv(LevelPool.load(C5), B, dev, **kw)
     b = SafeLifeVecEnv(LevelPool.load(C5), B, dev, **kw)
     b._state.board_planes = None         # the uint16-only form
@@ -208,7 +208,7 @@ def test_plane_mode_views_match_uint16_views(torch_dev, view, rw):
     B, T = 384, 40
     kw = dict(time_limit=11, view_shape=view, penalty_coef=1.0, min_performance=0.01,
               rng="philox", seed=5, level_order="random", augment_roll=True, kernel="fast",
-              output_channels=None, remove_white_goals=rw)
+              output_channels=None, remove_white_goals=rw, board_mode="planes")
     a = SafeLifeVecEnv(LevelPool.load(C5), B, dev, **kw)
     b = SafeLifeVecEnv(LevelPool.load(C5), B, dev, **kw)
     b._state.board_planes = None
@@ -228,4 +228,38 @@ def test_plane_mode_views_match_uint16_views(torch_dev, view, rw):
         if t >= 2:      # the boards stay in planes when the view is fused
             inp = int(((a.planes_ok & 64) != 0).sum().item())
             assert (inp > B // 2) if fused else inp == 0, (t, inp)
+    _same_state(a, b, "end")
+
+
+def test_board_mode_auto_follows_reads(torch_dev):
+    """board_mode="auto": a batch whose board is read after every step runs the kernel
+    that writes the uint16 board (no env left in planes, so a read costs no sync); once
+    the reads stop it goes back into plane mode.  Every output equals the uint16-only
+    form's throughout."""
+    from safelife_amd import SafeLifeVecEnv, LevelPool
+    torch, dev = torch_dev
+    B = 256
+    kw = dict(time_limit=13, view_shape=(33, 33), penalty_coef=1.0, min_performance=0.01,
+              rng="philox", seed=17, level_order="random", augment_roll=True, kernel="fast",
+              output_channels=None)
+    a = SafeLifeVecEnv(LevelPool.load(C5), B, dev, board_mode="auto", **kw)
+    b = SafeLifeVecEnv(LevelPool.load(C5), B, dev, board_mode="uint16", **kw)
+    a.reset()
+    b.reset()
+    rng = np.random.RandomState(3)
+    for t in range(36):
+        acts = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+        oa, ra, da, _ = a.step(acts)
+        ob, rb, db, _ = b.step(acts)
+        assert torch.equal(ra, rb) and torch.equal(da, db) and torch.equal(oa, ob), t
+        inp = int(((a.planes_ok & 64) != 0).sum().item())
+        assert int(((b.planes_ok & 64) != 0).sum().item()) == 0
+        if t < 12:                    # no reads yet: plane mode
+            assert inp > B // 2, t
+        elif t < 24:                  # reads after every step: the uint16 kernel
+            if t >= 13:
+                assert inp == 0, t
+            assert torch.equal(a.board, b.board), t
+        elif t >= 24 + a.BOARD_READ_WINDOW + 1:
+            assert inp > B // 2, t    # back in planes
     _same_state(a, b, "end")

@@ -37,7 +37,8 @@ def test_pool_feeder_swap_matches_set_pool(torch_dev, pool_name):
     first, second = full.subset(range(0, n1)), full.subset(range(n1, n2))
     B, T, swap_at = 64, 90, 30
     kw = dict(time_limit=20, view_shape=(9, 9), output_channels=None, penalty_coef=1.0,
-              min_performance=0.01, rng="philox", seed=4, kernel="auto")
+              min_performance=0.01, rng="philox", seed=4, kernel="auto",
+              board_mode="planes")      # (128x128: boards in planes between the reads)
     a = SafeLifeVecEnv(first, B, dev, **kw)
     b = SafeLifeVecEnv(first, B, dev, **kw)
     a.reset()
