@@ -398,36 +398,43 @@ __device__ __forceinline__ void view_band(u32 P[32], const u32 gcol[3][2], int t
 // The exits of the view (recenter_view's move_to_perimeter): every exit cell goes to
 // its clipped position, the last exit in np.nonzero order winning a shared one.  An
 // exit's value is the epilogue's (LEVEL_EXIT, red when the level can be exited: exits
-// are frozen and never change otherwise) plus its goal colour; the goal cell is read
-// past the vector L1 (this wave stored the goals' changed rows).
-__device__ __forceinline__ void view_exits(const sl_env_state &st, int64_t b, int agy, int agx,
-                                           int can) {
+// are frozen and never change otherwise) plus its goal colour.  The targets and the goal
+// cells are loaded before the epilogue (in flight with its loads); the goal cell past
+// the vector L1 (this wave stored the goals' changed rows, and waited for them).
+struct ViewExit {
+    int tgt;            // this lane's exit's view cell (-1: no exit, or a later one wins)
+    u32 goal;           // its goal cell
+};
+__device__ __forceinline__ ViewExit view_exits_load(const sl_env_state &st, int64_t b, int agy,
+                                                    int agx) {
     const Step128KArgs &k = kargs128();
     const int vh = k.fx.obs_vh, vw = k.fx.obs_vw;
     const int ne = min(__builtin_amdgcn_readfirstlane(st.exit_count[b]), SL_MAX_EXITS);
-    if (ne <= 0) return;
     const int lane = lane_now();
-    int tgt = -1;
-    uint16_t val = 0;
+    ViewExit ve{-1, 0u};
     if (lane < ne) {
         const int iy = st.exit_y[b * SL_MAX_EXITS + lane], ix = st.exit_x[b * SL_MAX_EXITS + lane];
         int jy = pymod(iy - agy + N / 2, N) - N / 2;
         int jx = pymod(ix - agx + N / 2, N) - N / 2;
         jy = min(max(jy + vh / 2, 0), vh - 1);
         jx = min(max(jx + vw / 2, 0), vw - 1);
-        tgt = jy * vw + jx;
+        ve.tgt = jy * vw + jx;
         const int ci = iy * N + ix;
         const u32 *gw = reinterpret_cast<const u32 *>(st.goals + b * (int64_t)(N * N)) + (ci >> 1);
-        const u32 g2 = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u32 ev = LEVEL_EXIT | (can ? COLOR_R : 0u);
-        val = obs::obs_value(ev, (g2 >> (16 * (ci & 1))) & 0xFFFFu, k.fx.obs_rw);
+        ve.goal = __hip_atomic_load(gw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (16 * (ci & 1));
     }
-    bool last = lane < ne;
-    for (int j = 1; j < ne; j++) {
-        const int tj = __builtin_amdgcn_readlane(tgt, j);
-        if (j > lane && tj == tgt) last = false;
+    for (int j = 1; j < ne; j++) {        // a later exit on the same cell wins
+        const int tj = __builtin_amdgcn_readlane(ve.tgt, j);
+        if (j > lane && tj == ve.tgt) ve.tgt = -1;
     }
-    if (last) k.fx.obs_out[b * (int64_t)(vh * vw) + tgt] = val;
+    return ve;
+}
+__device__ __forceinline__ void view_exits_store(const ViewExit &ve, int64_t b, int can) {
+    const Step128KArgs &k = kargs128();
+    if (ve.tgt < 0) return;
+    const u32 ev = LEVEL_EXIT | (can ? COLOR_R : 0u);
+    k.fx.obs_out[b * (int64_t)(k.fx.obs_vh * k.fx.obs_vw) + ve.tgt] =
+        obs::obs_value(ev, ve.goal & 0xFFFFu, k.fx.obs_rw);
 }
 
 // One env-step of env b, after the action: k_env_action has applied it -- state and cell edits in HBM, reward
@@ -795,10 +802,7 @@ __device__ __forceinline__ void step128_body(const Step128KArgs &ka) {
                 if (VIEW) transpose32(P);        // (a step into plane mode: planes again)
             }
         }
-        if (VIEW) {             // (the colour words again, from L2: not held through the stores)
-            band_gcol(gp, mg, t, sdy, sdx, gcol);
-            view_band(P, gcol, t, agy, agx, spool, b);
-        }
+        if (VIEW) view_band(P, gcol, t, agy, agx, spool, b);
     }
     if (MODE == SPAWN_DECIDED) {
         u32 E0[8];
@@ -821,6 +825,7 @@ __device__ __forceinline__ void step128_body(const Step128KArgs &ka) {
     // the epilogue's inputs, loaded now (in flight with the row stores) rather than held
     // through the bands: the reward, the bonus term and the record again (L2)
     const Step128KArgs &k = kargs128();
+    const ViewExit vex = VIEW ? view_exits_load(k.st, b, agy, agx) : ViewExit{-1, 0u};
     const u32 VE = load_record(k.st, k.actions, b, lane_now());
     const int act_reward = (int)scratch_of(k.fx.scratch, k.st.B).act[b];
     RecFields fl{VE, rec(VE, R_GO), rec(VE, R_AX), rec(VE, R_AY), 0.0};
@@ -843,7 +848,7 @@ __device__ __forceinline__ void step128_body(const Step128KArgs &ka) {
         }
     }
     // (the view's band stores have completed: wait_vm above)
-    if (VIEW) view_exits(k.st, b, agy, agx, __builtin_amdgcn_readfirstlane(can));
+    if (VIEW) view_exits_store(vex, b, __builtin_amdgcn_readfirstlane(can));
 }
 
 // the step kernel: Philox, the stream fallback or decided replay; no views

@@ -834,10 +834,7 @@ int launch_reset_list_wide(const sl_env_state &st, const sl_level_pool &pool, co
 
 extern "C" const char *sl_version(void) { return "safelife-hip 0.2 (gfx950)"; }
 
-#ifndef SL_BUILD_ID
-#define SL_BUILD_ID "unknown"
-#endif
-extern "C" const char *sl_build_id(void) { return SL_BUILD_ID; }
+// sl_build_id(): sl_buildid.cpp, compiled with every link (the hash of all sources)
 
 extern "C" int sl_device_arch(char *buf, int len) {
     int dev;
