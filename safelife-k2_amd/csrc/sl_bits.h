@@ -379,9 +379,11 @@ __device__ __forceinline__ int stream_draws(const u32 elig[2], u32 sp[2], double
 // stays lean.  Each 3x3 quantity is folded vertically (rows y-1, y, y+1) and then
 // horizontally (word 0 sees columns col0-1 .. col0+1; word 1 sees col0 .. col0+2),
 // one quantity at a time so only the reduced results stay live.
+// held (optional): the changed cells that held a bit of a plane other than 0, 3, 9-11
+// before the step (the planes a change clears but never sets), for plane-mode stores
 template <class Geo>
 __device__ __forceinline__ void rule_planes(u32 P[32], u32 chg[2], Geo &&g, const SpawnCtx &sc,
-                                            u32 tensor) {
+                                            u32 tensor, u32 *held = nullptr) {
     u32 eq3[2], eq34[2];
     {   // 9-cell alive count: 3-row sums s = s0 + 2 s1, then t0 + 2h over 3 columns
         u32 s0[2], s1[2];
@@ -481,6 +483,14 @@ __device__ __forceinline__ void rule_planes(u32 P[32], u32 chg[2], Geo &&g, cons
         const u32 c = kill[w] | birth[w] | sp[w];
         const u32 born = birth[w] | sp[w];
         chg[w] = c;
+        if (held) {
+            u32 o = PL(P, 1, w) | PL(P, 2, w);
+#pragma unroll
+            for (int k = 4; k <= 8; k++) o |= PL(P, k, w);
+#pragma unroll
+            for (int k = 12; k <= 15; k++) o |= PL(P, k, w);
+            held[w] = o & c;
+        }
         PL(P, 0, w) ^= c;
         PL(P, 3, w) = mux(c, (birth[w] & pairD[w]) | sp[w], PL(P, 3, w));
 #pragma unroll

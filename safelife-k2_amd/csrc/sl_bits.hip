@@ -803,6 +803,319 @@ k_env_step_bits64(StepKArgs ka) {
                         pre);
 }
 
+// ---------------------------------------------------------------- plane mode
+// The 64x64 board kept in bit planes across steps (round 6; the 128x128 kernel's
+// round-5 design, sl_bits128.hip): half 0 of the goals mirror (sl_env_state.planes:
+// word q of lane l at planes[b*4096 + q*64 + l] = plane q & 15 of column 2 (l >> 1) +
+// (q >> 4), rows 32 (l & 1) .. +31; half 1 keeps the goals).  A Philox step without
+// views or capture (sl_env_state.board_planes == planes) reads the plane words instead
+// of the uint16 board -- no transposes -- and stores only the words that changed.
+// planes_ok bit 6: the planes hold the board; bit 7: so does the uint16 board (after a
+// sync); bits 16-31: planes all zero for this env, neither loaded nor stored (the C3 /
+// C4 levels never use cell bits 7 and 11-14: 5 of the 16 planes, 31 % of the board's
+// bytes).  Of the uint16 board a plane step keeps only what the next step's action reads
+// (act_core: row agent_y, and column agent_x in rows agent_y +- 1, 2) and the exit
+// cells (the epilogue).
+constexpr int kPok64Board = 64, kPok64Full = 128, kPok64ZeroShift = 16;
+
+// The cells act_core can read around (y0, x0) -- the row within +-2 columns, the
+// column within +-2 rows -- loaded by lanes 0..8 (cell k in lane k), so the lane-0
+// action waits on one round trip, not on a chain of them; a cell is a v_readlane (it
+// reads the lane whatever the exec mask)
+struct NearCells {
+    int y0, x0;
+    u32 v;              // lane k: 0 centre; 1-4 columns -1, +1, -2, +2; 5-8 rows -1, +1, -2, +2
+    __device__ __forceinline__ uint32_t operator()(int i) const {
+        const int dy = (((i >> 6) - y0 + 32) & 63) - 32, dx = (((i & 63) - x0 + 32) & 63) - 32;
+        const int k = dy == 0 ? (dx == 0 ? 0 : dx == -1 ? 1 : dx == 1 ? 2 : dx == -2 ? 3 : 4)
+                              : (dy == -1 ? 5 : dy == 1 ? 6 : dy == -2 ? 7 : 8);
+        return (u32)__builtin_amdgcn_readlane((int)v, __builtin_amdgcn_readfirstlane(k));
+    }
+};
+__device__ __forceinline__ int near_cell_index(int k, int y0, int x0) {
+    const int dy = k < 5 ? 0 : (k == 5 ? -1 : k == 6 ? 1 : k == 7 ? -2 : 2);
+    const int dx = k >= 5 || k == 0 ? 0 : (k == 1 ? -1 : k == 2 ? 1 : k == 3 ? -2 : 2);
+    return ((y0 + dy) & 63) * 64 + ((x0 + dx) & 63);
+}
+
+// the board's plane words that are not known zero, DMA'd into the wave's buffer
+// (word q of lane l at buf[q * 64 + l]); no registers held while they are in flight
+__device__ __forceinline__ void dma_planes(const u32 *__restrict__ bp, u32 zero, lds_u32 *buf,
+                                           int lane) {
+#pragma unroll
+    for (int q = 0; q < 32; q++)
+        if (!((zero >> (q & 15)) & 1u))
+            __builtin_amdgcn_global_load_lds((const void *)(bp + q * 64 + lane),
+                                             (__attribute__((address_space(3))) void *)(buf + q * 64),
+                                             4, 0, 2);
+}
+
+// the cells of row y (whole) and of column x in rows y +- 1, 2 from the planes, into the
+// uint16 board: what the next step's action reads
+__device__ __forceinline__ void store_near_cells(const u32 P[32], int y, int x, u32 *gb_row0,
+                                                 uint16_t *cells, int lane) {
+    const int h = lane & 1, j = lane >> 1;
+    if ((y >> 5) == h) {            // row y: bit y & 31 of every word of this half's lanes
+        const u32 r = (u32)(y & 31);
+        u32 d = 0u;
+#pragma unroll
+        for (int k = 0; k < 32; k++) d |= ((P[k] >> r) & 1u) << k;
+        __builtin_nontemporal_store(d, gb_row0 + y * 32 + j);
+    }
+#pragma unroll
+    for (int dd = 0; dd < 4; dd++) {
+        const int yy = (y + (dd < 2 ? dd - 2 : dd - 1)) & 63;
+        if (lane == 2 * (x >> 1) + (yy >> 5)) {
+            const u32 r = (u32)(yy & 31);
+            u32 v = 0u;
+            if (x & 1) {
+#pragma unroll
+                for (int p = 0; p < 16; p++) v |= ((PL(P, p, 1) >> r) & 1u) << p;
+            } else {
+#pragma unroll
+                for (int p = 0; p < 16; p++) v |= ((PL(P, p, 0) >> r) & 1u) << p;
+            }
+            cells[yy * 64 + x] = (uint16_t)v;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64, kMinWaves)
+k_env_step_bits64_planes(StepKArgs ka) {
+    const sl_env_state &st = ka.st;
+    const StepArgs &a = ka.a;
+    const FastExtra &fx = ka.fx;
+    const int64_t b = blockIdx.x;          // one wave per env
+    const int lane = threadIdx.x;
+    __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
+    lds_u32 *buf = (lds_u32 *)&stage[0];
+    Pre pre;
+    issue_pre(st, ka.actions, b, lane, pre);
+    const int64_t off = b * (int64_t)(N * N);
+    const int lane_off = (lane & 1) * 1024 + (lane >> 1);     // dwords: row 32h, column pair j
+    u32 *gg = reinterpret_cast<u32 *>(st.goals + off) + lane_off;
+    u32 *mg = st.planes + b * 4096 + 2048 + lane;
+    u32 *bp = st.planes + b * 4096 + lane;
+    const u32 V = pre.V;
+    const int pok_all = rec(V, R_POK);
+    const bool pin = (pok_all & kPok64Board) != 0;
+    const u32 zero = pin ? ((u32)pok_all >> kPok64ZeroShift) : 0u;    // planes known zero
+    // the board: its planes, or (a step into plane mode) its rows
+    if (pin) dma_planes(st.planes + b * 4096, zero, buf, lane);
+    else dma_board(st.board + off, buf, lane);
+    // the cells the action reads, around the pre-action agent
+    const int ay0 = rec(V, R_AY), ax0 = rec(V, R_AX);
+    const u32 near = lane < 9 ? (u32)st.board[off + near_cell_index(lane, ay0, ax0)] : 0u;
+    u32 gcol[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        gcol[k][0] = pre.g[k][0];
+        gcol[k][1] = pre.g[k][1];
+    }
+    const int pok = pok_all & 6;
+    int gok = pok;                 // the goals' planes_ok bits after this step
+
+    SpawnCtx sc;
+    sc.gid = a.env0 + (uint32_t)b;
+    sc.step = a.step;
+    sc.seed = a.seed;
+    set_spawn_prob(sc, __int_as_float(rec(V, R_SPAWN)));
+    const StreamSrc ssrc{a.draws, a.n_draws, nullptr, a.draw_mask, a.draw_bits};
+
+    // ---- goals (as in step_env: the mirror in half 1, the fixed-point skip)
+    if ((pok & 6) != 6) {
+        u32 PG[32];
+        if (pok & 2) {
+#pragma unroll
+            for (int q = 0; q < 32; q++) PG[q] = mg[q * 64];
+        } else {
+            load_pairs_nt<32>(gg, PG);
+            transpose32(PG);
+        }
+        u32 cg[2];
+        rule_planes(PG, cg, Geo64<SPAWN_PHILOX>{lane, ssrc, 0, 0}, sc, 1u);
+        const u32 rg = wave_or(cg[0] | cg[1]);
+        const bool all = !(pok & 2);
+#pragma unroll
+        for (int w = 0; w < 2; w++)
+            if (all || cg[w])
+#pragma unroll
+                for (int k = 0; k < 16; k++) mg[(k + 16 * w) * 64] = PL(PG, k, w);
+        const bool fixed = rg == 0 && __ballot((PL(PG, 7, 0) | PL(PG, 7, 1)) != 0u) == 0ull;
+        gok = 2 | (fixed ? 4 : 0);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            gcol[k][0] = PL(PG, 9 + k, 0);
+            gcol[k][1] = PL(PG, 9 + k, 1);
+        }
+        if (rg) {
+            transpose32(PG);
+#pragma unroll
+            for (int y = 0; y < 32; y++)
+                if ((rg >> y) & 1u) __builtin_nontemporal_store(PG[y], &gg[y * 32]);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    int roll = -1;
+    if (fx.pool.K > 0 && fx.pool.board_planes && st.start_roll) roll = rec(V, R_ROLL);
+    // the action (lane 0) on the cells round the agent
+    NearCells nc;
+    nc.y0 = ay0;
+    nc.x0 = ax0;
+    nc.v = near;
+    OverlayT<NearCells> ov;
+    ov.src = nc;
+    ov.n = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        ov.idx[k] = 0;
+        ov.val[k] = 0;
+    }
+    RecEnv env{st, b, rec(V, R_GO), ax0, ay0, rec(V, R_SCORE), rec(V, R_BASE), rec(V, R_POSS),
+               rec_f64(V, R_MP)};
+    int act_reward = 0;
+    if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
+    act_reward = __builtin_amdgcn_readfirstlane(act_reward);
+    const int ne = __builtin_amdgcn_readfirstlane(ov.n);
+    int eidx[4];
+    u32 eval[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        eidx[k] = __builtin_amdgcn_readfirstlane(ov.idx[k]);
+        eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
+    }
+    RecFields fl{V, __builtin_amdgcn_readfirstlane(env.go), __builtin_amdgcn_readfirstlane(env.ax),
+                 __builtin_amdgcn_readfirstlane(env.ay), 0.0};
+    if (a.bonus_period > 0)        // issued now, consumed by the epilogue
+        fl.bval = a.bonus_table[bonus_dist(fl.ax, fl.ay, fl.prior_x(fl.prior_head()),
+                                           fl.prior_y(fl.prior_head()), fl.prior_len(),
+                                           a.bonus_period, a.bonus_len)];
+
+    u32 PB[32];
+    wait_vm();                      // the DMA has landed
+    if (pin) {
+#pragma unroll
+        for (int q = 0; q < 32; q++) PB[q] = ((zero >> (q & 15)) & 1u) ? 0u : buf[q * 64 + lane];
+    } else {
+        read_pairs(buf, lane, PB);
+    }
+    wait_lgkm();
+    if (roll < 0) dma_board(st.start_board + off, buf, lane);
+    else pool_dma(fx.pool, rec(V, R_LI), buf, lane);
+    if (!pin) transpose32(PB);
+    // the action's edits into the planes (their words are stored whole below)
+    (void)mux_edits(PB, ne, eidx, eval, lane);
+    // held: changed cells that held a plane a change clears but never sets
+    u32 cb[2], held[2];
+    rule_planes(PB, cb, Geo64<SPAWN_PHILOX>{lane, ssrc, 0, 0}, sc, 0u, held);
+    // (a lane mask, not two words held through the scores: such a lane stores those
+    // planes for every changed word)
+    const uint64_t held_lanes = __ballot((held[0] | held[1]) != 0u);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- scores over the new board and goals
+    u32 PS[32];
+    wait_vm();
+    if (roll >= 0) {
+        pool_planes_lds(buf, roll >> 16, roll & 0xFFFF, lane, PS);
+    } else {
+        read_pairs(buf, lane, PS);
+        transpose32(PS);
+    }
+    int pts, scr, pos, side;
+    score_planes(PB, gcol, PS, &pts, &scr, &pos, &side);
+    const int s1 = wave_total((pts + 192) | ((scr + 64) << 16));
+    const int s2 = wave_total(pos | (side << 16));
+    __builtin_amdgcn_sched_barrier(0);
+    const int points = (s1 & 0xFFFF) - 192 * 64;
+    const int score = ((s1 >> 16) & 0xFFFF) - 64 * 64;
+    const int possible = s2 & 0xFFFF;
+    const int side_total = (s2 >> 16) & 0xFFFF;
+
+    // ---- exits in the colour the epilogue gives them (update_exit_colors), then the
+    // plane words that changed
+    const bool can = can_exit_now(fl.min_performance(), score, fl.baseline(), possible);
+    u32 d9[2];
+#pragma unroll
+    for (int w = 0; w < 2; w++) {
+        const u32 o9 = PL(PB, 9, w);
+        PL(PB, 9, w) = can ? (o9 | PL(PB, 8, w)) : (o9 & ~PL(PB, 8, w));
+        d9[w] = o9 ^ PL(PB, 9, w);
+    }
+    u32 nzl = 0u;                   // this lane's nonzero planes
+#pragma unroll
+    for (int k = 0; k < 16; k++) nzl |= ((PL(PB, k, 0) | PL(PB, k, 1)) != 0u ? 1u : 0u) << k;
+    const u32 nz = wave_or(nzl);
+    const u32 fresh = pin ? (nz & zero) : nz;       // stored whole: not in HBM as they are
+    u32 em[2] = {0u, 0u};           // the words the action's edits touched (this lane's)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (k < ne) {
+            const int y = eidx[k] >> 6, x = eidx[k] & 63;
+            const u32 bit = lane == 2 * (x >> 1) + (y >> 5) ? 1u << (y & 31) : 0u;
+            em[x & 1] |= bit;
+        }
+    }
+    u32 dw[2], dall[2];
+#pragma unroll
+    for (int w = 0; w < 2; w++) {
+        dw[w] = cb[w] | em[w];                       // words whose cells changed
+        dall[w] = em[w] | (((held_lanes >> lane) & 1ull) ? cb[w] : 0u);   // ... other planes
+    }
+    if (fresh || wave_or(dw[0] | dw[1] | d9[0] | d9[1])) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            if (!((nz >> k) & 1u)) continue;         // all zero now (bit set below)
+            const bool whole = (fresh >> k) & 1u;
+#pragma unroll
+            for (int w = 0; w < 2; w++) {
+                const u32 d = (k == 0 || k == 3 || k == 10 || k == 11) ? dw[w]
+                              : k == 9 ? (dw[w] | d9[w]) : dall[w];
+                if (whole || d) __builtin_nontemporal_store(PL(PB, k, w), &bp[(k + 16 * w) * 64]);
+            }
+        }
+    }
+    // what the next action reads, in the uint16 board
+    store_near_cells(PB, fl.ay, fl.ax, reinterpret_cast<u32 *>(st.board + off),
+                     st.board + off, lane);
+    const int ok = gok | kPok64Board | (int)((~nz & 0xFFFFu) << kPok64ZeroShift);
+    if (ok != pok_all && lane == 0) st.planes_ok[b] = ok;
+    int reset = 0;
+    if (lane == 0)
+        reset = epilogue_core(st, a, b, fl, act_reward, points, score, possible, side_total,
+                              ka.reward_out, ka.done_out, ka.flags_out, ka.ep_len_out,
+                              ka.ep_rew_out);
+    reset = __builtin_amdgcn_readfirstlane(reset);
+    if (fx.fuse_reset && reset && lane == 0) {
+        int64_t *cnt = fx.scratch + 8 * st.B + 2 + (a.step & 1);
+        const int i = (int)atomicAdd((unsigned long long *)cnt, 1ull);
+        reset_list(fx.scratch)[i] = (int32_t)b;
+    }
+}
+
+// sl_env_board_sync for 64x64 boards in planes: one wave per env
+__global__ void __launch_bounds__(64) k_board_sync64(sl_env_state st, int demote) {
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int pok = __builtin_amdgcn_readfirstlane(st.planes_ok[b]);
+    if (!(pok & kPok64Board)) return;
+    if (!(pok & kPok64Full)) {
+        const u32 zero = (u32)pok >> kPok64ZeroShift;
+        const u32 *bp = st.planes + b * 4096 + lane;
+        u32 P[32];
+#pragma unroll
+        for (int q = 0; q < 32; q++) P[q] = ((zero >> (q & 15)) & 1u) ? 0u : bp[q * 64];
+        transpose32(P);
+        u32 *gb = reinterpret_cast<u32 *>(st.board + b * (int64_t)(N * N)) + (lane & 1) * 1024 +
+                  (lane >> 1);
+#pragma unroll
+        for (int y = 0; y < 32; y++) gb[y * 32] = P[y];
+    }
+    if (lane == 0)
+        st.planes_ok[b] = demote ? pok & 0x3F : pok | kPok64Full;
+}
+
 // Replay-mode count of env b (SL_RNG_STREAM), one wave, after k_env_action (one lane
 // per env) has applied the actions -- state and cell edits in HBM, rewards in scratch
 // act[] -- so the board read here is the acted-on one: the eligible cells, i.e. the
@@ -918,6 +1231,16 @@ void launch_bits64(int kind, unsigned grid, const StepKArgs &ka, hipStream_t s) 
 
 namespace sl {
 
+bool planes64_shape(const sl_env_state &st) {
+    return st.H == N && st.W == N && st.planes && st.planes_ok && st.board_planes == st.planes;
+}
+
+int sync_board_planes64(const sl_env_state &st, int demote, hipStream_t s) {
+    if (!planes64_shape(st) || st.B <= 0) return SL_OK;
+    hipLaunchKernelGGL(k_board_sync64, dim3((unsigned)st.B), dim3(64), 0, s, st, demote);
+    return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
+}
+
 int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra &fx,
                      const int32_t *actions, int ctp, int ctc, double *reward, uint8_t *done,
                      uint8_t *flags, int32_t *ep_len, int32_t *ep_rew, hipStream_t s) {
@@ -939,7 +1262,10 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         launch_bits64<SPAWN_STREAM>(obs_kind(fx), grid, ka, s);
     } else {
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        launch_bits64<SPAWN_PHILOX>(obs_kind(fx), grid, ka, s);
+        if (fx.plane_mode)
+            hipLaunchKernelGGL(k_env_step_bits64_planes, dim3(grid), dim3(64), 0, s, ka);
+        else
+            launch_bits64<SPAWN_PHILOX>(obs_kind(fx), grid, ka, s);
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);

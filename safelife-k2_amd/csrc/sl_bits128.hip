@@ -1419,6 +1419,7 @@ bool bits128_shape(const sl_env_state &st) {
 }
 
 int sync_board_planes(const sl_env_state &st, int demote, hipStream_t s) {
+    if (st.H == 64) return sync_board_planes64(st, demote, s);
     if (!st.board_planes || !st.planes_ok || st.H != N || st.W != N || st.B <= 0) return SL_OK;
     hipLaunchKernelGGL(k_board_sync128, dim3((unsigned)st.B), dim3(64), 0, s, st, demote);
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;

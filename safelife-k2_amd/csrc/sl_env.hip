@@ -1045,7 +1045,12 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
                              oa.vh <= kViewMaxRows128 && oa.vw <= 128;
     fx.plane_mode = (fast128 && planes128 && (!cfg->obs_out || fuse_obs128) && !cap &&
                      (!replay || st->elig_planes) && cfg->board_mode != SL_BOARD_UINT16) ? 1 : 0;
-    if (planes128 && !fx.plane_mode) {
+    // 64x64: a Philox step without views or capture (sl_bits.hip, plane mode)
+    const bool planes64 = planes64_shape(*st);
+    if (planes64)
+        fx.plane_mode = (fast && !cfg->obs_out && !cap && !replay &&
+                         cfg->board_mode != SL_BOARD_UINT16) ? 1 : 0;
+    if ((planes128 || planes64) && !fx.plane_mode) {
         const int rc = sync_board_planes(*st, 1, s);
         if (rc) return rc;
     }

@@ -386,6 +386,10 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
 // kept in planes; demote: then mark the planes stale (before a step or edit that
 // works on the uint16 board).  No-op unless the state has board planes.
 int sync_board_planes(const sl_env_state &st, int demote, hipStream_t s);
+// 64x64 (sl_bits.hip): plane mode when st.board_planes == st.planes (the board in half
+// 0 of the goals mirror); the sync of such a state
+bool planes64_shape(const sl_env_state &st);
+int sync_board_planes64(const sl_env_state &st, int demote, hipStream_t s);
 int launch_env_action(const sl_env_state &st, const int32_t *actions, int ctp, int ctc,
                       int64_t *act, hipStream_t s);
 // resets of the envs queued in the scratch list for step `step`, one 1024-thread

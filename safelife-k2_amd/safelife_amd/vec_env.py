@@ -197,6 +197,11 @@ class SafeLifeVecEnv:
             s.planes = self.planes.data_ptr()
             s.planes_ok = self.planes_ok.data_ptr()
         self.board_planes = None
+        if (H, W) == (64, 64):
+            # the 64x64 board's planes share the goals mirror's tensor (half 0; the goals
+            # use half 1): board_planes == planes selects plane mode (sl_bits.hip)
+            self.board_planes = self.planes
+            s.board_planes = self.planes.data_ptr()
         if (H, W) == (128, 128):
             # the 128x128 board in bit planes, kept there by steps without observations
             # (sl_env_state.board_planes); `board` completes the uint16 tensor when it
