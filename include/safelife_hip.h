@@ -389,7 +389,19 @@ typedef struct sl_env_state {
                                  points that read or write st->board do so
                                  themselves.  A caller that writes the uint16
                                  board clears planes_ok (as for the goals
-                                 mirror).                                      */
+                                 mirror).  64x64: board_planes == planes puts
+                                 the board's planes in half 0 of the goals
+                                 mirror (Philox steps without views; bit 7
+                                 only after a sync or a reset).                */
+    uint32_t board_zero;      /* 64x64 plane mode: cell bits (planes) that are
+                                 0 in every board of the batch and that no rule,
+                                 action or reset can set (the caller's promise:
+                                 none in its levels or written boards, not
+                                 LIFE / COLOR_R, not toggled powers / colours);
+                                 their planes are neither loaded nor stored.
+                                 To widen it, complete the board first
+                                 (sl_env_board_sync) and clear planes_ok bits
+                                 6-7.  0 = every plane.                        */
 } sl_env_state;
 
 /* A device-resident level pool (the level_iterator's levels). */

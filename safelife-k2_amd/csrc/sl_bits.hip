@@ -808,38 +808,18 @@ k_env_step_bits64(StepKArgs ka) {
 // round-5 design, sl_bits128.hip): half 0 of the goals mirror (sl_env_state.planes:
 // word q of lane l at planes[b*4096 + q*64 + l] = plane q & 15 of column 2 (l >> 1) +
 // (q >> 4), rows 32 (l & 1) .. +31; half 1 keeps the goals).  A Philox step without
-// views or capture (sl_env_state.board_planes == planes) reads the plane words instead
-// of the uint16 board -- no transposes -- and stores only the words that changed.
-// planes_ok bit 6: the planes hold the board; bit 7: so does the uint16 board (after a
-// sync); bits 16-31: planes all zero for this env, neither loaded nor stored (the C3 /
-// C4 levels never use cell bits 7 and 11-14: 5 of the 16 planes, 31 % of the board's
-// bytes).  Of the uint16 board a plane step keeps only what the next step's action reads
-// (act_core: row agent_y, and column agent_x in rows agent_y +- 1, 2) and the exit
-// cells (the epilogue).
-constexpr int kPok64Board = 64, kPok64Full = 128, kPok64ZeroShift = 16;
+// views or capture (sl_env_state.board_planes == planes) DMA's the plane words into
+// the wave's buffer at once -- as the uint16 board was -- runs the action on them, and
+// stores only the words that changed; no transposes.  Planes in
+// sl_env_state.board_zero (all zero in every board of the batch, for good: the C3 / C4
+// pools never use cell bits 7 and 11-14, 31 % of the board's bytes) are neither loaded
+// nor stored.  planes_ok bit 6: the planes hold the board; bit 7: so does the uint16
+// board (a sync, or a reset, wrote it), which a plane step otherwise leaves stale
+// (exits aside: the epilogue writes them in both).
+constexpr int kPok64Board = 64, kPok64Full = 128;
 
-// The cells act_core can read around (y0, x0) -- the row within +-2 columns, the
-// column within +-2 rows -- loaded by lanes 0..8 (cell k in lane k), so the lane-0
-// action waits on one round trip, not on a chain of them; a cell is a v_readlane (it
-// reads the lane whatever the exec mask)
-struct NearCells {
-    int y0, x0;
-    u32 v;              // lane k: 0 centre; 1-4 columns -1, +1, -2, +2; 5-8 rows -1, +1, -2, +2
-    __device__ __forceinline__ uint32_t operator()(int i) const {
-        const int dy = (((i >> 6) - y0 + 32) & 63) - 32, dx = (((i & 63) - x0 + 32) & 63) - 32;
-        const int k = dy == 0 ? (dx == 0 ? 0 : dx == -1 ? 1 : dx == 1 ? 2 : dx == -2 ? 3 : 4)
-                              : (dy == -1 ? 5 : dy == 1 ? 6 : dy == -2 ? 7 : 8);
-        return (u32)__builtin_amdgcn_readlane((int)v, __builtin_amdgcn_readfirstlane(k));
-    }
-};
-__device__ __forceinline__ int near_cell_index(int k, int y0, int x0) {
-    const int dy = k < 5 ? 0 : (k == 5 ? -1 : k == 6 ? 1 : k == 7 ? -2 : 2);
-    const int dx = k >= 5 || k == 0 ? 0 : (k == 1 ? -1 : k == 2 ? 1 : k == 3 ? -2 : 2);
-    return ((y0 + dy) & 63) * 64 + ((x0 + dx) & 63);
-}
-
-// the board's plane words that are not known zero, DMA'd into the wave's buffer
-// (word q of lane l at buf[q * 64 + l]); no registers held while they are in flight
+// the board's plane words outside `zero`, DMA'd into the wave's buffer (word q of
+// lane l at buf[q * 64 + l]); no registers held while they are in flight
 __device__ __forceinline__ void dma_planes(const u32 *__restrict__ bp, u32 zero, lds_u32 *buf,
                                            int lane) {
 #pragma unroll
@@ -850,35 +830,22 @@ __device__ __forceinline__ void dma_planes(const u32 *__restrict__ bp, u32 zero,
                                              4, 0, 2);
 }
 
-// the cells of row y (whole) and of column x in rows y +- 1, 2 from the planes, into the
-// uint16 board: what the next step's action reads
-__device__ __forceinline__ void store_near_cells(const u32 P[32], int y, int x, u32 *gb_row0,
-                                                 uint16_t *cells, int lane) {
-    const int h = lane & 1, j = lane >> 1;
-    if ((y >> 5) == h) {            // row y: bit y & 31 of every word of this half's lanes
+// unedited cells for the action from the staged planes: cell (y, x) is bit y & 31 of
+// word p + 16 (x & 1) of lane 2 (x >> 1) + (y >> 5); planes in `zero` are 0
+struct LdsPlaneCells {
+    const lds_u32 *buf;
+    u32 zero;
+    __device__ __forceinline__ uint32_t operator()(int i) const {
+        const int y = i >> 6, x = i & 63;
+        const lds_u32 *q = buf + (16 * (x & 1)) * 64 + 2 * (x >> 1) + (y >> 5);
         const u32 r = (u32)(y & 31);
-        u32 d = 0u;
+        uint32_t v = 0;
 #pragma unroll
-        for (int k = 0; k < 32; k++) d |= ((P[k] >> r) & 1u) << k;
-        __builtin_nontemporal_store(d, gb_row0 + y * 32 + j);
+        for (int p = 0; p < 16; p++)
+            if (!((zero >> p) & 1u)) v |= ((q[p * 64] >> r) & 1u) << p;
+        return v;
     }
-#pragma unroll
-    for (int dd = 0; dd < 4; dd++) {
-        const int yy = (y + (dd < 2 ? dd - 2 : dd - 1)) & 63;
-        if (lane == 2 * (x >> 1) + (yy >> 5)) {
-            const u32 r = (u32)(yy & 31);
-            u32 v = 0u;
-            if (x & 1) {
-#pragma unroll
-                for (int p = 0; p < 16; p++) v |= ((PL(P, p, 1) >> r) & 1u) << p;
-            } else {
-#pragma unroll
-                for (int p = 0; p < 16; p++) v |= ((PL(P, p, 0) >> r) & 1u) << p;
-            }
-            cells[yy * 64 + x] = (uint16_t)v;
-        }
-    }
-}
+};
 
 __global__ void __launch_bounds__(64, kMinWaves)
 k_env_step_bits64_planes(StepKArgs ka) {
@@ -889,8 +856,12 @@ k_env_step_bits64_planes(StepKArgs ka) {
     const int lane = threadIdx.x;
     __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
     lds_u32 *buf = (lds_u32 *)&stage[0];
+    const u32 zero = st.board_zero & 0xFFFFu;
     Pre pre;
     issue_pre(st, ka.actions, b, lane, pre);
+    // the board's planes, speculatively: an env whose planes do not hold its board (the
+    // first step after a host write or a step in another mode) reloads its rows below
+    dma_planes(st.planes + b * 4096, zero, buf, lane);
     const int64_t off = b * (int64_t)(N * N);
     const int lane_off = (lane & 1) * 1024 + (lane >> 1);     // dwords: row 32h, column pair j
     u32 *gg = reinterpret_cast<u32 *>(st.goals + off) + lane_off;
@@ -899,13 +870,6 @@ k_env_step_bits64_planes(StepKArgs ka) {
     const u32 V = pre.V;
     const int pok_all = rec(V, R_POK);
     const bool pin = (pok_all & kPok64Board) != 0;
-    const u32 zero = pin ? ((u32)pok_all >> kPok64ZeroShift) : 0u;    // planes known zero
-    // the board: its planes, or (a step into plane mode) its rows
-    if (pin) dma_planes(st.planes + b * 4096, zero, buf, lane);
-    else dma_board(st.board + off, buf, lane);
-    // the cells the action reads, around the pre-action agent
-    const int ay0 = rec(V, R_AY), ax0 = rec(V, R_AX);
-    const u32 near = lane < 9 ? (u32)st.board[off + near_cell_index(lane, ay0, ax0)] : 0u;
     u32 gcol[3][2];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -959,31 +923,57 @@ k_env_step_bits64_planes(StepKArgs ka) {
 
     int roll = -1;
     if (fx.pool.K > 0 && fx.pool.board_planes && st.start_roll) roll = rec(V, R_ROLL);
-    // the action (lane 0) on the cells round the agent
-    NearCells nc;
-    nc.y0 = ay0;
-    nc.x0 = ax0;
-    nc.v = near;
-    OverlayT<NearCells> ov;
-    ov.src = nc;
-    ov.n = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        ov.idx[k] = 0;
-        ov.val[k] = 0;
+    wait_vm();
+    if (!pin) {                     // a step into plane mode: the uint16 board instead
+        dma_board(st.board + off, buf, lane);
+        wait_vm();
     }
-    RecEnv env{st, b, rec(V, R_GO), ax0, ay0, rec(V, R_SCORE), rec(V, R_BASE), rec(V, R_POSS),
-               rec_f64(V, R_MP)};
+    // the action (lane 0) on the staged board
+    RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
+               rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     int act_reward = 0;
-    if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
-    act_reward = __builtin_amdgcn_readfirstlane(act_reward);
-    const int ne = __builtin_amdgcn_readfirstlane(ov.n);
+    int ne = 0;
     int eidx[4];
     u32 eval[4];
+    if (pin) {
+        OverlayT<LdsPlaneCells> ov;
+        ov.src = LdsPlaneCells{buf, zero};
+        ov.n = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            ov.idx[k] = 0;
+            ov.val[k] = 0;
+        }
+        if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
+        ne = ov.n;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            eidx[k] = ov.idx[k];
+            eval[k] = ov.val[k];
+        }
+    } else {
+        OverlayT<LdsCells> ov;
+        ov.src.buf = buf;
+        ov.n = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            ov.idx[k] = 0;
+            ov.val[k] = 0;
+        }
+        if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
+        ne = ov.n;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            eidx[k] = ov.idx[k];
+            eval[k] = ov.val[k];
+        }
+    }
+    act_reward = __builtin_amdgcn_readfirstlane(act_reward);
+    ne = __builtin_amdgcn_readfirstlane(ne);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        eidx[k] = __builtin_amdgcn_readfirstlane(ov.idx[k]);
-        eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)ov.val[k]);
+        eidx[k] = __builtin_amdgcn_readfirstlane(eidx[k]);
+        eval[k] = (u32)__builtin_amdgcn_readfirstlane((int)eval[k]);
     }
     RecFields fl{V, __builtin_amdgcn_readfirstlane(env.go), __builtin_amdgcn_readfirstlane(env.ax),
                  __builtin_amdgcn_readfirstlane(env.ay), 0.0};
@@ -993,7 +983,6 @@ k_env_step_bits64_planes(StepKArgs ka) {
                                            a.bonus_period, a.bonus_len)];
 
     u32 PB[32];
-    wait_vm();                      // the DMA has landed
     if (pin) {
 #pragma unroll
         for (int q = 0; q < 32; q++) PB[q] = ((zero >> (q & 15)) & 1u) ? 0u : buf[q * 64 + lane];
@@ -1004,7 +993,6 @@ k_env_step_bits64_planes(StepKArgs ka) {
     if (roll < 0) dma_board(st.start_board + off, buf, lane);
     else pool_dma(fx.pool, rec(V, R_LI), buf, lane);
     if (!pin) transpose32(PB);
-    // the action's edits into the planes (their words are stored whole below)
     (void)mux_edits(PB, ne, eidx, eval, lane);
     // held: changed cells that held a plane a change clears but never sets
     u32 cb[2], held[2];
@@ -1034,7 +1022,7 @@ k_env_step_bits64_planes(StepKArgs ka) {
     const int side_total = (s2 >> 16) & 0xFFFF;
 
     // ---- exits in the colour the epilogue gives them (update_exit_colors), then the
-    // plane words that changed
+    // plane words that changed (all of them on a step into plane mode)
     const bool can = can_exit_now(fl.min_performance(), score, fl.baseline(), possible);
     u32 d9[2];
 #pragma unroll
@@ -1043,11 +1031,6 @@ k_env_step_bits64_planes(StepKArgs ka) {
         PL(PB, 9, w) = can ? (o9 | PL(PB, 8, w)) : (o9 & ~PL(PB, 8, w));
         d9[w] = o9 ^ PL(PB, 9, w);
     }
-    u32 nzl = 0u;                   // this lane's nonzero planes
-#pragma unroll
-    for (int k = 0; k < 16; k++) nzl |= ((PL(PB, k, 0) | PL(PB, k, 1)) != 0u ? 1u : 0u) << k;
-    const u32 nz = wave_or(nzl);
-    const u32 fresh = pin ? (nz & zero) : nz;       // stored whole: not in HBM as they are
     u32 em[2] = {0u, 0u};           // the words the action's edits touched (this lane's)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -1063,23 +1046,19 @@ k_env_step_bits64_planes(StepKArgs ka) {
         dw[w] = cb[w] | em[w];                       // words whose cells changed
         dall[w] = em[w] | (((held_lanes >> lane) & 1ull) ? cb[w] : 0u);   // ... other planes
     }
-    if (fresh || wave_or(dw[0] | dw[1] | d9[0] | d9[1])) {
+    if (!pin || wave_or(dw[0] | dw[1] | d9[0] | d9[1])) {
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-            if (!((nz >> k) & 1u)) continue;         // all zero now (bit set below)
-            const bool whole = (fresh >> k) & 1u;
+            if ((zero >> k) & 1u) continue;
 #pragma unroll
             for (int w = 0; w < 2; w++) {
                 const u32 d = (k == 0 || k == 3 || k == 10 || k == 11) ? dw[w]
                               : k == 9 ? (dw[w] | d9[w]) : dall[w];
-                if (whole || d) __builtin_nontemporal_store(PL(PB, k, w), &bp[(k + 16 * w) * 64]);
+                if (!pin || d) __builtin_nontemporal_store(PL(PB, k, w), &bp[(k + 16 * w) * 64]);
             }
         }
     }
-    // what the next action reads, in the uint16 board
-    store_near_cells(PB, fl.ay, fl.ax, reinterpret_cast<u32 *>(st.board + off),
-                     st.board + off, lane);
-    const int ok = gok | kPok64Board | (int)((~nz & 0xFFFFu) << kPok64ZeroShift);
+    const int ok = gok | kPok64Board;
     if (ok != pok_all && lane == 0) st.planes_ok[b] = ok;
     int reset = 0;
     if (lane == 0)
@@ -1101,7 +1080,7 @@ __global__ void __launch_bounds__(64) k_board_sync64(sl_env_state st, int demote
     const int pok = __builtin_amdgcn_readfirstlane(st.planes_ok[b]);
     if (!(pok & kPok64Board)) return;
     if (!(pok & kPok64Full)) {
-        const u32 zero = (u32)pok >> kPok64ZeroShift;
+        const u32 zero = st.board_zero & 0xFFFFu;
         const u32 *bp = st.planes + b * 4096 + lane;
         u32 P[32];
 #pragma unroll
@@ -1113,7 +1092,7 @@ __global__ void __launch_bounds__(64) k_board_sync64(sl_env_state st, int demote
         for (int y = 0; y < 32; y++) gb[y * 32] = P[y];
     }
     if (lane == 0)
-        st.planes_ok[b] = demote ? pok & 0x3F : pok | kPok64Full;
+        st.planes_ok[b] = demote ? pok & ~(kPok64Board | kPok64Full) : pok | kPok64Full;
 }
 
 // Replay-mode count of env b (SL_RNG_STREAM), one wave, after k_env_action (one lane

@@ -129,7 +129,9 @@ class SafeLifeGame:
 
     @board.setter
     def board(self, value):
-        self._venv.board[self._idx].copy_(self._upload(value))
+        v = self._upload(value)
+        self._venv._allow_board_bits(self._venv._device_board_bits(v))
+        self._venv.board[self._idx].copy_(v)
         self._set("spawn_flags", self._st("spawn_flags") | 1)   # may now hold a spawner
         self._venv._may_spawn = True
         # bit 3: the board's draw planes (128x128 replay) described the old board;
@@ -426,6 +428,7 @@ class SafeLifeGame:
         pool = LevelPool.from_levels([lvl])
         pdev = pool.to_device(v.device)
         v._may_spawn = v._may_spawn or pool.has_spawners()
+        v._allow_board_bits(v._pool_bits(pool))      # (64x64 planes kept zero)
         cfg = v._fill_cfg()
         cfg.level_mode, cfg.augment_roll, cfg.env0, cfg.n_total_envs = 0, 0, 0, 1
         cfg.wrapper_min_performance = float("nan")

@@ -202,6 +202,7 @@ class SafeLifeVecEnv:
             # use half 1): board_planes == planes selects plane mode (sl_bits.hip)
             self.board_planes = self.planes
             s.board_planes = self.planes.data_ptr()
+            s.board_zero = self._zero_planes(self._pool_bits(self.pool))
         if (H, W) == (128, 128):
             # the 128x128 board in bit planes, kept there by steps without observations
             # (sl_env_state.board_planes); `board` completes the uint16 tensor when it
@@ -240,6 +241,41 @@ class SafeLifeVecEnv:
         self._pool_dev = self.pool.to_device(self.device)
         self._cfg = _lib.EnvCfg()
 
+    # ------------------------------------------------- 64x64 planes that stay zero
+    @staticmethod
+    def _pool_bits(pool):
+        return int(np.bitwise_or.reduce(pool.board.reshape(-1))) if pool.board.size else 0
+
+    def _zero_planes(self, bits):
+        """sl_env_state.board_zero: the cell bits no board of this batch can hold -- none
+        in its boards (`bits`), not set by a birth or a spawn (LIFE, colours present), an
+        exit (COLOR_R) or a toggle (powers / colours when they can be toggled)."""
+        can = bits | 0x0009 | 0x0200
+        if self.can_toggle_powers:
+            can |= 0x00E1
+        if self.can_toggle_colors:
+            can |= 0x0E00
+        return (~can) & 0xFFFF
+
+    def _allow_board_bits(self, bits):
+        """Boards with cell bits `bits` are about to enter the batch: planes that must now
+        be loaded and stored leave board_zero.  Envs kept in planes under the old mask are
+        completed and taken out of plane mode first (their planes in the new mask's
+        complement were never written)."""
+        s = self._state
+        if not s.board_zero:
+            return
+        new = s.board_zero & self._zero_planes(bits)
+        if new != s.board_zero:
+            self.sync_board()
+            self.planes_ok.bitwise_and_(~(64 | 128))
+            s.board_zero = new
+
+    def _device_board_bits(self, boards):
+        """OR of every cell of a uint16 device tensor (16 reductions; rare events only)."""
+        v = boards.view(self.torch.int16)
+        return sum(1 << k for k in range(16) if bool(((v >> k) & 1).any().item()))
+
     def set_pool(self, levels, pool_dev=None):
         """Replace the level pool the next resets draw from (same board shape).
 
@@ -252,6 +288,7 @@ class SafeLifeVecEnv:
                              % (pool.H, pool.W, self.H, self.W))
         if pool.K < 1:
             raise ValueError("empty level pool")
+        self._allow_board_bits(self._pool_bits(pool))
         self.pool = pool
         self._pool_dev = pool_dev if pool_dev is not None else pool.to_device(self.device)
         self._check_ring_threshold(pool.spawn_prob)
@@ -695,6 +732,9 @@ class SafeLifeVecEnv:
         s.B, s.H, s.W = n, self.H, self.W
         for name, _ in _lib.EnvState._fields_[3:]:
             base = getattr(full, name)
+            if name == "board_zero":          # (a mask, not a per-env pointer)
+                s.board_zero = base
+                continue
             if not base:
                 setattr(s, name, None)
                 continue
@@ -759,6 +799,8 @@ class SafeLifeVecEnv:
         longer match pool levels (kernels read them from HBM), the bit-plane
         mirrors are stale and the reset lists start empty."""
         self.st_t["start_roll"].fill_(-1)
+        if self._state.board_zero:      # boards written from outside: their bits count
+            self._state.board_zero &= self._zero_planes(self._device_board_bits(self._board))
         # may hold spawners (replay counts them); bit 2 (128x128 boards): the start board
         # uses cell bits 12-14, which the 128x128 kernel then compares in a second pass
         hi = start_board_hi_bits(self.start_board) & ((self.H, self.W) == (128, 128))

@@ -1,9 +1,9 @@
 """The 64x64 board kept in bit planes (round 6; sl_bits.hip k_env_step_bits64_planes).
 
 A Philox step without views or capture keeps the board in half 0 of the goals
-mirror, skips the planes that are all zero for an env (planes_ok bits 16-31; on the
-C3 / C4 levels cell bits 7 and 11-14), stores only the plane words that changed, and
-keeps of the uint16 board only the cells the next action reads.  One batch in plane
+mirror, skips the planes no board of the batch can hold (sl_env_state.board_zero; on
+the C3 / C4 levels cell bits 7 and 11-14), stores only the plane words that changed,
+and leaves the uint16 board stale (a read completes it).  One batch in plane
 mode and one in the uint16-only form run side by side from the same seed; every
 output must be equal at every step, through resets, board reads between plane steps,
 steps with views (back to the uint16 board), set_state, the game-level C entries and
@@ -124,22 +124,46 @@ def test_plane_mode64_matches_uint16_mode(torch_dev, name):
             b.set_state(b.board.cpu().numpy(), b.goals.cpu().numpy(),
                         b.start_board.cpu().numpy())
     # the last step was a plane step: check the planes themselves, then the board
-    pok = a.planes_ok.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    pok = a.planes_ok.cpu().numpy()
     bp = a.planes.cpu().numpy().view(np.uint32).reshape(B, 2, 32, 64)[:, 0]
     bd = a.board.cpu().numpy()          # (completes the uint16 board; planes unchanged)
     inp = np.nonzero(pok & 64)[0]
     assert len(inp) > B // 2
-    zeros_seen = 0
+    zero = a._state.board_zero
+    assert zero == (0x7880 if name != "spawners" else 0x7000), hex(zero)
     for e in inp[:96]:
         hp = _host_planes64(bd[e])
-        zero = (pok[e] >> 16) & 0xFFFF
         for q in range(32):
             if (zero >> (q & 15)) & 1:
-                assert not hp[q].any(), (e, q)      # a plane marked zero is zero
-                zeros_seen += 1
+                assert not hp[q].any(), (e, q)      # a plane kept zero is zero
             else:
                 assert np.array_equal(bp[e, q], hp[q]), (e, q)
-    assert zeros_seen > 0
+    _same_state(a, b, "end")
+
+
+def test_plane_mode64_pool_swap_widens_zero_planes(torch_dev):
+    """set_pool with levels holding cell bits the batch never had (spawners, blue) takes
+    the planes out of board_zero: the envs in planes are completed and leave plane mode
+    first, and everything stays equal to the uint16 form before and after."""
+    from safelife_amd import LevelPool
+    torch, dev = torch_dev
+    B = 384
+    a, b = _pair(torch_dev, LevelPool.load(C3), B, seed=23, tl=9)
+    assert a._state.board_zero == 0x7880
+    rng = np.random.RandomState(12)
+    sp = _spawner_pool()
+    for t in range(40):
+        if t == 15:
+            a.set_pool(sp)
+            b.set_pool(sp)
+            assert a._state.board_zero == 0x7000
+            assert int(((a.planes_ok & 64) != 0).sum().item()) == 0
+        acts = torch.from_numpy(rng.randint(0, 9, size=B).astype(np.int32)).to(dev)
+        a.step_async(acts)
+        b.step_async(acts)
+        for x, y in ((a.reward, b.reward), (a.done, b.done), (a.flags, b.flags)):
+            assert torch.equal(x, y), t
+    assert int(((a.planes_ok & 64) != 0).sum().item()) > B // 2
     _same_state(a, b, "end")
 
 
