@@ -812,37 +812,57 @@ k_env_step_bits64(StepKArgs ka) {
 // the wave's buffer at once -- as the uint16 board was -- runs the action on them, and
 // stores only the words that changed; no transposes.  Planes in
 // sl_env_state.board_zero (all zero in every board of the batch, for good: the C3 / C4
-// pools never use cell bits 7 and 11-14, 31 % of the board's bytes) are neither loaded
-// nor stored.  planes_ok bit 6: the planes hold the board; bit 7: so does the uint16
+// pools never use cell bits 7 and 11-14) are neither loaded nor stored, and the kept
+// ones are packed (PlaneSlots): 6 of the 8 KiB are read.  planes_ok bit 6: the planes hold the board; bit 7: so does the uint16
 // board (a sync, or a reset, wrote it), which a plane step otherwise leaves stale
 // (exits aside: the epilogue writes them in both).
 constexpr int kPok64Board = 64, kPok64Full = 128;
 
-// the board's plane words outside `zero`, DMA'd into the wave's buffer (word q of
-// lane l at buf[q * 64 + l]); no registers held while they are in flight
-__device__ __forceinline__ void dma_planes(const u32 *__restrict__ bp, u32 zero, lds_u32 *buf,
+// The planes outside `zero` packed word after word: word q (plane q & 15 of column
+// word q >> 4) at position pos(q), the number of kept words below it, so the kept words
+// come first and one DMA instruction of 16 B per lane moves four of them (C3: 22 of 32
+// words in 6 instructions, where 4-B DMAs word by word took 22 and ran 12 % slower).
+// The layout follows sl_env_state.board_zero, which changes only after every board has
+// left the planes.
+struct PlaneSlots {
+    u32 keep;           // bit q: word q is kept
+    __device__ __forceinline__ bool kept(int q) const { return (keep >> q) & 1u; }
+    __device__ __forceinline__ int pos(int q) const {
+        return __builtin_popcount(keep & ((1u << q) - 1u));
+    }
+    static __device__ __forceinline__ PlaneSlots of(u32 zero) {
+        return PlaneSlots{(~zero & 0xFFFFu) * 0x10001u};
+    }
+};
+
+// the kept plane words of an env, DMA'd into the wave's buffer in their packed order
+// (position p of lane l at buf[p * 64 + l]); no registers held while they are in flight
+__device__ __forceinline__ void dma_planes(const u32 *__restrict__ bp, PlaneSlots ps, lds_u32 *buf,
                                            int lane) {
+    const int groups = (__builtin_popcount(ps.keep) + 3) >> 2;
+    const char *s = reinterpret_cast<const char *>(bp);
 #pragma unroll
-    for (int q = 0; q < 32; q++)
-        if (!((zero >> (q & 15)) & 1u))
-            __builtin_amdgcn_global_load_lds((const void *)(bp + q * 64 + lane),
-                                             (__attribute__((address_space(3))) void *)(buf + q * 64),
-                                             4, 0, 2);
+    for (int g = 0; g < 8; g++)
+        if (g < groups)
+            __builtin_amdgcn_global_load_lds((const void *)(s + g * 1024 + lane * 16),
+                                             (__attribute__((address_space(3))) void *)(buf + g * 256),
+                                             16, 0, 2);
 }
 
 // unedited cells for the action from the staged planes: cell (y, x) is bit y & 31 of
-// word p + 16 (x & 1) of lane 2 (x >> 1) + (y >> 5); planes in `zero` are 0
+// word p + 16 (x & 1) of lane 2 (x >> 1) + (y >> 5); planes not kept are 0
 struct LdsPlaneCells {
     const lds_u32 *buf;
-    u32 zero;
+    PlaneSlots ps;
     __device__ __forceinline__ uint32_t operator()(int i) const {
         const int y = i >> 6, x = i & 63;
-        const lds_u32 *q = buf + (16 * (x & 1)) * 64 + 2 * (x >> 1) + (y >> 5);
+        const lds_u32 *q = buf + 2 * (x >> 1) + (y >> 5);
         const u32 r = (u32)(y & 31);
+        const int w = 16 * (x & 1);
         uint32_t v = 0;
 #pragma unroll
         for (int p = 0; p < 16; p++)
-            if (!((zero >> p) & 1u)) v |= ((q[p * 64] >> r) & 1u) << p;
+            if (ps.kept(p)) v |= ((q[ps.pos(p + w) * 64] >> r) & 1u) << p;
         return v;
     }
 };
@@ -856,12 +876,12 @@ k_env_step_bits64_planes(StepKArgs ka) {
     const int lane = threadIdx.x;
     __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
     lds_u32 *buf = (lds_u32 *)&stage[0];
-    const u32 zero = st.board_zero & 0xFFFFu;
+    const PlaneSlots ps = PlaneSlots::of(st.board_zero);
     Pre pre;
     issue_pre(st, ka.actions, b, lane, pre);
     // the board's planes, speculatively: an env whose planes do not hold its board (the
     // first step after a host write or a step in another mode) reloads its rows below
-    dma_planes(st.planes + b * 4096, zero, buf, lane);
+    dma_planes(st.planes + b * 4096, ps, buf, lane);
     const int64_t off = b * (int64_t)(N * N);
     const int lane_off = (lane & 1) * 1024 + (lane >> 1);     // dwords: row 32h, column pair j
     u32 *gg = reinterpret_cast<u32 *>(st.goals + off) + lane_off;
@@ -937,7 +957,7 @@ k_env_step_bits64_planes(StepKArgs ka) {
     u32 eval[4];
     if (pin) {
         OverlayT<LdsPlaneCells> ov;
-        ov.src = LdsPlaneCells{buf, zero};
+        ov.src = LdsPlaneCells{buf, ps};
         ov.n = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -985,7 +1005,7 @@ k_env_step_bits64_planes(StepKArgs ka) {
     u32 PB[32];
     if (pin) {
 #pragma unroll
-        for (int q = 0; q < 32; q++) PB[q] = ((zero >> (q & 15)) & 1u) ? 0u : buf[q * 64 + lane];
+        for (int q = 0; q < 32; q++) PB[q] = ps.kept(q) ? buf[ps.pos(q) * 64 + lane] : 0u;
     } else {
         read_pairs(buf, lane, PB);
     }
@@ -1049,12 +1069,13 @@ k_env_step_bits64_planes(StepKArgs ka) {
     if (!pin || wave_or(dw[0] | dw[1] | d9[0] | d9[1])) {
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-            if ((zero >> k) & 1u) continue;
+            if (!ps.kept(k)) continue;
 #pragma unroll
             for (int w = 0; w < 2; w++) {
                 const u32 d = (k == 0 || k == 3 || k == 10 || k == 11) ? dw[w]
                               : k == 9 ? (dw[w] | d9[w]) : dall[w];
-                if (!pin || d) __builtin_nontemporal_store(PL(PB, k, w), &bp[(k + 16 * w) * 64]);
+                if (!pin || d)
+                    __builtin_nontemporal_store(PL(PB, k, w), &bp[ps.pos(k + 16 * w) * 64]);
             }
         }
     }
@@ -1080,11 +1101,11 @@ __global__ void __launch_bounds__(64) k_board_sync64(sl_env_state st, int demote
     const int pok = __builtin_amdgcn_readfirstlane(st.planes_ok[b]);
     if (!(pok & kPok64Board)) return;
     if (!(pok & kPok64Full)) {
-        const u32 zero = st.board_zero & 0xFFFFu;
+        const PlaneSlots ps = PlaneSlots::of(st.board_zero);
         const u32 *bp = st.planes + b * 4096 + lane;
         u32 P[32];
 #pragma unroll
-        for (int q = 0; q < 32; q++) P[q] = ((zero >> (q & 15)) & 1u) ? 0u : bp[q * 64];
+        for (int q = 0; q < 32; q++) P[q] = ps.kept(q) ? bp[ps.pos(q) * 64] : 0u;
         transpose32(P);
         u32 *gb = reinterpret_cast<u32 *>(st.board + b * (int64_t)(N * N)) + (lane & 1) * 1024 +
                   (lane >> 1);

@@ -131,13 +131,15 @@ def test_plane_mode64_matches_uint16_mode(torch_dev, name):
     assert len(inp) > B // 2
     zero = a._state.board_zero
     assert zero == (0x7880 if name != "spawners" else 0x7000), hex(zero)
+    keep = ((~zero) & 0xFFFF) * 0x10001        # the kept words, packed (PlaneSlots)
     for e in inp[:96]:
         hp = _host_planes64(bd[e])
         for q in range(32):
             if (zero >> (q & 15)) & 1:
                 assert not hp[q].any(), (e, q)      # a plane kept zero is zero
             else:
-                assert np.array_equal(bp[e, q], hp[q]), (e, q)
+                pos = bin(keep & ((1 << q) - 1)).count("1")
+                assert np.array_equal(bp[e, pos], hp[q]), (e, q)
     _same_state(a, b, "end")
 
 
@@ -163,7 +165,8 @@ def test_plane_mode64_pool_swap_widens_zero_planes(torch_dev):
         b.step_async(acts)
         for x, y in ((a.reward, b.reward), (a.done, b.done), (a.flags, b.flags)):
             assert torch.equal(x, y), t
-    assert int(((a.planes_ok & 64) != 0).sum().item()) > B // 2
+        if t == 35:                # (between two rounds of resets) back in planes
+            assert int(((a.planes_ok & 64) != 0).sum().item()) > B // 2
     _same_state(a, b, "end")
 
 
