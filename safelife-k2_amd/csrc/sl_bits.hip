@@ -827,8 +827,11 @@ constexpr int kPok64Board = 64, kPok64Full = 128;
 struct PlaneSlots {
     u32 keep;           // bit q: word q is kept
     __device__ __forceinline__ bool kept(int q) const { return (keep >> q) & 1u; }
+    // (recomputed where used: two SALU, not 32 positions held in SGPRs all kernel long)
     __device__ __forceinline__ int pos(int q) const {
-        return __builtin_popcount(keep & ((1u << q) - 1u));
+        u32 k = keep;
+        asm volatile("" : "+s"(k));
+        return __builtin_popcount(k & ((1u << q) - 1u));
     }
     static __device__ __forceinline__ PlaneSlots of(u32 zero) {
         return PlaneSlots{(~zero & 0xFFFFu) * 0x10001u};
@@ -849,23 +852,39 @@ __device__ __forceinline__ void dma_planes(const u32 *__restrict__ bp, PlaneSlot
                                              16, 0, 2);
 }
 
-// unedited cells for the action from the staged planes: cell (y, x) is bit y & 31 of
-// word p + 16 (x & 1) of lane 2 (x >> 1) + (y >> 5); planes not kept are 0
-struct LdsPlaneCells {
-    const lds_u32 *buf;
-    PlaneSlots ps;
+// The cells act_core can read around (y0, x0) -- the row within +-2 columns, the
+// column within +-2 rows: near_cell_index(k) -- gathered from the staged planes by
+// lanes 0..8 at once (16 LDS reads for the wave, not 16 per cell on the action's lane),
+// then read by the lane-0 action with v_readlane (whatever the exec mask)
+__device__ __forceinline__ int near_cell_index(int k, int y0, int x0) {
+    const int dy = k < 5 ? 0 : (k == 5 ? -1 : k == 6 ? 1 : k == 7 ? -2 : 2);
+    const int dx = k >= 5 || k == 0 ? 0 : (k == 1 ? -1 : k == 2 ? 1 : k == 3 ? -2 : 2);
+    return ((y0 + dy) & 63) * 64 + ((x0 + dx) & 63);
+}
+struct NearCells {
+    int y0, x0;
+    u32 v;              // lane k: cell near_cell_index(k)
     __device__ __forceinline__ uint32_t operator()(int i) const {
-        const int y = i >> 6, x = i & 63;
-        const lds_u32 *q = buf + 2 * (x >> 1) + (y >> 5);
-        const u32 r = (u32)(y & 31);
-        const int w = 16 * (x & 1);
-        uint32_t v = 0;
-#pragma unroll
-        for (int p = 0; p < 16; p++)
-            if (ps.kept(p)) v |= ((q[ps.pos(p + w) * 64] >> r) & 1u) << p;
-        return v;
+        const int dy = (((i >> 6) - y0 + 32) & 63) - 32, dx = (((i & 63) - x0 + 32) & 63) - 32;
+        const int k = dy == 0 ? (dx == 0 ? 0 : dx == -1 ? 1 : dx == 1 ? 2 : dx == -2 ? 3 : 4)
+                              : (dy == -1 ? 5 : dy == 1 ? 6 : dy == -2 ? 7 : 8);
+        return (u32)__builtin_amdgcn_readlane((int)v, __builtin_amdgcn_readfirstlane(k));
     }
 };
+// cell i from the staged planes (this lane's; planes not kept are 0)
+__device__ __forceinline__ u32 lds_plane_cell(const lds_u32 *buf, PlaneSlots ps, int i) {
+    const int y = i >> 6, x = i & 63;
+    const lds_u32 *q = buf + 2 * (x >> 1) + (y >> 5);
+    const u32 r = (u32)(y & 31);
+    const int w = 16 * (x & 1);
+    u32 v = 0;
+#pragma unroll
+    for (int p = 0; p < 16; p++) {
+        const int pw = ps.pos(p) + (w ? __builtin_popcount(ps.keep & 0xFFFFu) : 0);
+        if (ps.kept(p)) v |= ((q[pw * 64] >> r) & 1u) << p;
+    }
+    return v;
+}
 
 __global__ void __launch_bounds__(64, kMinWaves)
 k_env_step_bits64_planes(StepKArgs ka) {
@@ -956,8 +975,10 @@ k_env_step_bits64_planes(StepKArgs ka) {
     int eidx[4];
     u32 eval[4];
     if (pin) {
-        OverlayT<LdsPlaneCells> ov;
-        ov.src = LdsPlaneCells{buf, ps};
+        const int ay0 = rec(V, R_AY), ax0 = rec(V, R_AX);
+        const u32 near = lane < 9 ? lds_plane_cell(buf, ps, near_cell_index(lane, ay0, ax0)) : 0u;
+        OverlayT<NearCells> ov;
+        ov.src = NearCells{ay0, ax0, near};
         ov.n = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
