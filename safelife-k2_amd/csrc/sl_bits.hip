@@ -824,25 +824,34 @@ constexpr int kPok64Board = 64, kPok64Full = 128;
 // words in 6 instructions, where 4-B DMAs word by word took 22 and ran 12 % slower).
 // The layout follows sl_env_state.board_zero, which changes only after every board has
 // left the planes.
+template <u32 K16>       // the kept planes, fixed at compile time; 0: from board_zero
 struct PlaneSlots {
-    u32 keep;           // bit q: word q is kept
-    __device__ __forceinline__ bool kept(int q) const { return (keep >> q) & 1u; }
-    // (recomputed where used: two SALU, not 32 positions held in SGPRs all kernel long)
+    u32 keep;           // bit q: word q is kept (K16 == 0)
+    __device__ __forceinline__ u32 keep32() const { return K16 ? K16 * 0x10001u : keep; }
+    __device__ __forceinline__ bool kept(int q) const { return (keep32() >> q) & 1u; }
+    // (at run time recomputed where used: two SALU, not 32 positions held in SGPRs all
+    // kernel long; with K16 a constant)
     __device__ __forceinline__ int pos(int q) const {
+        if (K16) return __builtin_popcount((K16 * 0x10001u) & ((1u << q) - 1u));
         u32 k = keep;
         asm volatile("" : "+s"(k));
         return __builtin_popcount(k & ((1u << q) - 1u));
     }
+    __device__ __forceinline__ int kept16() const { return __builtin_popcount(keep32() & 0xFFFFu); }
     static __device__ __forceinline__ PlaneSlots of(u32 zero) {
         return PlaneSlots{(~zero & 0xFFFFu) * 0x10001u};
     }
 };
+// the instantiations: every plane, the C3 / C4 pools' planes (cell bits 0-6, 8-10, 15),
+// and any other mask at run time
+constexpr u32 kKeepAll = 0xFFFFu, kKeepC3 = 0x877Fu;
 
 // the kept plane words of an env, DMA'd into the wave's buffer in their packed order
 // (position p of lane l at buf[p * 64 + l]); no registers held while they are in flight
-__device__ __forceinline__ void dma_planes(const u32 *__restrict__ bp, PlaneSlots ps, lds_u32 *buf,
-                                           int lane) {
-    const int groups = (__builtin_popcount(ps.keep) + 3) >> 2;
+template <u32 K16>
+__device__ __forceinline__ void dma_planes(const u32 *__restrict__ bp, PlaneSlots<K16> ps,
+                                           lds_u32 *buf, int lane) {
+    const int groups = (2 * ps.kept16() + 3) >> 2;
     const char *s = reinterpret_cast<const char *>(bp);
 #pragma unroll
     for (int g = 0; g < 8; g++)
@@ -872,7 +881,8 @@ struct NearCells {
     }
 };
 // cell i from the staged planes (this lane's; planes not kept are 0)
-__device__ __forceinline__ u32 lds_plane_cell(const lds_u32 *buf, PlaneSlots ps, int i) {
+template <u32 K16>
+__device__ __forceinline__ u32 lds_plane_cell(const lds_u32 *buf, PlaneSlots<K16> ps, int i) {
     const int y = i >> 6, x = i & 63;
     const lds_u32 *q = buf + 2 * (x >> 1) + (y >> 5);
     const u32 r = (u32)(y & 31);
@@ -880,12 +890,13 @@ __device__ __forceinline__ u32 lds_plane_cell(const lds_u32 *buf, PlaneSlots ps,
     u32 v = 0;
 #pragma unroll
     for (int p = 0; p < 16; p++) {
-        const int pw = ps.pos(p) + (w ? __builtin_popcount(ps.keep & 0xFFFFu) : 0);
+        const int pw = ps.pos(p) + (w ? ps.kept16() : 0);
         if (ps.kept(p)) v |= ((q[pw * 64] >> r) & 1u) << p;
     }
     return v;
 }
 
+template <u32 K16>
 __global__ void __launch_bounds__(64, kMinWaves)
 k_env_step_bits64_planes(StepKArgs ka) {
     const sl_env_state &st = ka.st;
@@ -895,7 +906,7 @@ k_env_step_bits64_planes(StepKArgs ka) {
     const int lane = threadIdx.x;
     __shared__ __attribute__((aligned(16))) u32 stage[N * N / 2];
     lds_u32 *buf = (lds_u32 *)&stage[0];
-    const PlaneSlots ps = PlaneSlots::of(st.board_zero);
+    const PlaneSlots<K16> ps = PlaneSlots<K16>::of(st.board_zero);
     Pre pre;
     issue_pre(st, ka.actions, b, lane, pre);
     // the board's planes, speculatively: an env whose planes do not hold its board (the
@@ -963,51 +974,42 @@ k_env_step_bits64_planes(StepKArgs ka) {
     int roll = -1;
     if (fx.pool.K > 0 && fx.pool.board_planes && st.start_roll) roll = rec(V, R_ROLL);
     wait_vm();
-    if (!pin) {                     // a step into plane mode: the uint16 board instead
+    if (!pin) {
+        // a step into plane mode: the uint16 board instead, transposed and put into the
+        // buffer in the planes' layout, so everything below reads planes
         dma_board(st.board + off, buf, lane);
         wait_vm();
+        u32 R[32];
+        read_pairs(buf, lane, R);
+        transpose32(R);
+#pragma unroll
+        for (int q = 0; q < 32; q++)
+            if (ps.kept(q)) buf[ps.pos(q) * 64 + lane] = R[q];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
-    // the action (lane 0) on the staged board
+    // the action (lane 0) on the cells round the agent, gathered from the staged planes
     RecEnv env{st, b, rec(V, R_GO), rec(V, R_AX), rec(V, R_AY), rec(V, R_SCORE),
                rec(V, R_BASE), rec(V, R_POSS), rec_f64(V, R_MP)};
     int act_reward = 0;
-    int ne = 0;
     int eidx[4];
     u32 eval[4];
-    if (pin) {
-        const int ay0 = rec(V, R_AY), ax0 = rec(V, R_AX);
-        const u32 near = lane < 9 ? lds_plane_cell(buf, ps, near_cell_index(lane, ay0, ax0)) : 0u;
-        OverlayT<NearCells> ov;
-        ov.src = NearCells{ay0, ax0, near};
-        ov.n = 0;
+    const int ay0 = rec(V, R_AY), ax0 = rec(V, R_AX);
+    const u32 near = lane < 9 ? lds_plane_cell(buf, ps, near_cell_index(lane, ay0, ax0)) : 0u;
+    OverlayT<NearCells> ov;
+    ov.src = NearCells{ay0, ax0, near};
+    ov.n = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            ov.idx[k] = 0;
-            ov.val[k] = 0;
-        }
-        if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
-        ne = ov.n;
+    for (int k = 0; k < 4; k++) {
+        ov.idx[k] = 0;
+        ov.val[k] = 0;
+    }
+    if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
+    int ne = ov.n;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            eidx[k] = ov.idx[k];
-            eval[k] = ov.val[k];
-        }
-    } else {
-        OverlayT<LdsCells> ov;
-        ov.src.buf = buf;
-        ov.n = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            ov.idx[k] = 0;
-            ov.val[k] = 0;
-        }
-        if (lane == 0) act_reward = act_core(env, rec(V, R_ACT), N, N, ka.ctp, ka.ctc, ov);
-        ne = ov.n;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            eidx[k] = ov.idx[k];
-            eval[k] = ov.val[k];
-        }
+    for (int k = 0; k < 4; k++) {
+        eidx[k] = ov.idx[k];
+        eval[k] = ov.val[k];
     }
     act_reward = __builtin_amdgcn_readfirstlane(act_reward);
     ne = __builtin_amdgcn_readfirstlane(ne);
@@ -1024,16 +1026,11 @@ k_env_step_bits64_planes(StepKArgs ka) {
                                            a.bonus_period, a.bonus_len)];
 
     u32 PB[32];
-    if (pin) {
 #pragma unroll
-        for (int q = 0; q < 32; q++) PB[q] = ps.kept(q) ? buf[ps.pos(q) * 64 + lane] : 0u;
-    } else {
-        read_pairs(buf, lane, PB);
-    }
+    for (int q = 0; q < 32; q++) PB[q] = ps.kept(q) ? buf[ps.pos(q) * 64 + lane] : 0u;
     wait_lgkm();
     if (roll < 0) dma_board(st.start_board + off, buf, lane);
     else pool_dma(fx.pool, rec(V, R_LI), buf, lane);
-    if (!pin) transpose32(PB);
     (void)mux_edits(PB, ne, eidx, eval, lane);
     // held: changed cells that held a plane a change clears but never sets
     u32 cb[2], held[2];
@@ -1122,7 +1119,7 @@ __global__ void __launch_bounds__(64) k_board_sync64(sl_env_state st, int demote
     const int pok = __builtin_amdgcn_readfirstlane(st.planes_ok[b]);
     if (!(pok & kPok64Board)) return;
     if (!(pok & kPok64Full)) {
-        const PlaneSlots ps = PlaneSlots::of(st.board_zero);
+        const PlaneSlots<0> ps = PlaneSlots<0>::of(st.board_zero);
         const u32 *bp = st.planes + b * 4096 + lane;
         u32 P[32];
 #pragma unroll
@@ -1283,8 +1280,15 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         launch_bits64<SPAWN_STREAM>(obs_kind(fx), grid, ka, s);
     } else {
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        if (fx.plane_mode)
-            hipLaunchKernelGGL(k_env_step_bits64_planes, dim3(grid), dim3(64), 0, s, ka);
+        if (fx.plane_mode) {
+            const u32 keep = ~st.board_zero & 0xFFFFu;
+            if (keep == kKeepC3)
+                hipLaunchKernelGGL(k_env_step_bits64_planes<kKeepC3>, dim3(grid), dim3(64), 0, s, ka);
+            else if (keep == kKeepAll)
+                hipLaunchKernelGGL(k_env_step_bits64_planes<kKeepAll>, dim3(grid), dim3(64), 0, s, ka);
+            else
+                hipLaunchKernelGGL(k_env_step_bits64_planes<0>, dim3(grid), dim3(64), 0, s, ka);
+        }
         else
             launch_bits64<SPAWN_PHILOX>(obs_kind(fx), grid, ka, s);
     }
