@@ -402,6 +402,12 @@ typedef struct sl_env_state {
                                  To widen it, complete the board first
                                  (sl_env_board_sync) and clear planes_ok bits
                                  6-7.  0 = every plane.                        */
+    int32_t planes_live;      /* host flag, kept by the library: a plane-mode
+                                 step set it (some board may be in planes);
+                                 a demotion clears it.  While 0 the syncs the
+                                 entry points run are skipped.  Zero-init; a
+                                 caller stepping a slice (a copy of this
+                                 struct) ORs the slice's flag back in.         */
 } sl_env_state;
 
 /* A device-resident level pool (the level_iterator's levels). */

@@ -952,6 +952,19 @@ extern "C" int sl_env_reset(sl_env_state *st, const sl_level_pool *pool, const u
     return hipGetLastError() == hipSuccess ? SL_OK : SL_EHIP;
 }
 
+// The board planes' sync (sync_board_planes), skipped while no step of this state has
+// left a board in planes since the last demotion (sl_env_state.planes_live: a step that
+// is not in plane mode, e.g. with channel views, launched no-op syncs otherwise)
+static int sync_planes(const sl_env_state *st, hipStream_t s) {
+    return st->planes_live ? sync_board_planes(*st, 0, s) : SL_OK;
+}
+static int demote_planes(sl_env_state *st, hipStream_t s) {
+    if (!st->planes_live) return SL_OK;
+    const int rc = sync_board_planes(*st, 1, s);
+    if (!rc) st->planes_live = 0;
+    return rc;
+}
+
 extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const int32_t *actions,
                            const sl_env_cfg *cfg, double *reward, uint8_t *done,
                            uint8_t *info_flags, int32_t *ep_len, int32_t *ep_reward,
@@ -1051,9 +1064,11 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
         fx.plane_mode = (fast && !cfg->obs_out && !cap && !replay &&
                          cfg->board_mode != SL_BOARD_UINT16) ? 1 : 0;
     if ((planes128 || planes64) && !fx.plane_mode) {
-        const int rc = sync_board_planes(*st, 1, s);
+        const int rc = demote_planes(st, s);
         if (rc) return rc;
     }
+    // (a plane-mode step below leaves boards in planes)
+    if (fx.plane_mode && cfg->stream_phase != 1) st->planes_live = 1;
     // observations: packed views of 64x64 boards come out of the step kernel itself
     // ... and channel views too (one wave writes its env's 16-byte chunks from the
     // view masks it builds in LDS: views up to kFusedChanCells cells, 16-B aligned out)
@@ -1194,14 +1209,14 @@ extern "C" int sl_env_obs(const sl_env_state *st, int vh, int vw, int remove_whi
     ObsArgs a;
     int rc = obs_args(vh, vw, remove_white_goals, obs_mode, channels, nch, &a);
     if (rc) return rc;
-    rc = sync_board_planes(*st, 0, (hipStream_t)stream);
+    rc = sync_planes(st, (hipStream_t)stream);
     if (rc) return rc;
     return launch_obs(*st, a, out, (hipStream_t)stream);
 }
 
 extern "C" int sl_env_board_sync(sl_env_state *st, void *stream) {
     if (!state_ok(st)) return SL_EINVAL;
-    return sync_board_planes(*st, 0, (hipStream_t)stream);
+    return sync_planes(st, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -1211,7 +1226,7 @@ extern "C" int sl_env_action(sl_env_state *st, const int32_t *actions, int can_t
                              int can_toggle_colors, int64_t *act, void *stream) {
     if (!state_ok(st) || !actions || !act) return SL_EINVAL;
     if (st->B == 0) return SL_OK;
-    const int rc = sync_board_planes(*st, 1, (hipStream_t)stream);
+    const int rc = demote_planes(st, (hipStream_t)stream);
     if (rc) return rc;
     hipLaunchKernelGGL(k_env_action<true>, dim3((unsigned)((st->B + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, *st, actions, can_toggle_powers, can_toggle_colors,
@@ -1229,7 +1244,7 @@ extern "C" int sl_env_advance(sl_env_state *st, const sl_env_cfg *cfg, void *str
     const int64_t B = st->B;
     if (B == 0) return SL_OK;
     hipStream_t s = (hipStream_t)stream;
-    const int rcs = sync_board_planes(*st, 1, s);
+    const int rcs = demote_planes(st, s);
     if (rcs) return rcs;
     const Scratch sc = scratch_of(cfg->scratch, B);
     const size_t lds = (size_t)2 * st->H * st->W * sizeof(uint16_t);
@@ -1272,7 +1287,7 @@ extern "C" int sl_env_advance(sl_env_state *st, const sl_env_cfg *cfg, void *str
 extern "C" int sl_env_rescore(sl_env_state *st, int32_t *points, void *stream) {
     if (!state_ok(st)) return SL_EINVAL;
     if (st->B == 0) return SL_OK;
-    const int rc = sync_board_planes(*st, 0, (hipStream_t)stream);
+    const int rc = sync_planes(st, (hipStream_t)stream);
     if (rc) return rc;
     hipLaunchKernelGGL(k_env_rescore, dim3((unsigned)st->B), dim3(NT), 0, (hipStream_t)stream,
                        *st, points);
@@ -1282,7 +1297,7 @@ extern "C" int sl_env_rescore(sl_env_state *st, int32_t *points, void *stream) {
 extern "C" int sl_env_exit_colors(sl_env_state *st, int mode, void *stream) {
     if (!state_ok(st) || (mode != 0 && mode != 1)) return SL_EINVAL;
     if (st->B == 0) return SL_OK;
-    const int rc = sync_board_planes(*st, 1, (hipStream_t)stream);
+    const int rc = demote_planes(st, (hipStream_t)stream);
     if (rc) return rc;
     hipLaunchKernelGGL(k_env_exit_colors, dim3((unsigned)((st->B + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, *st, mode);

@@ -45,7 +45,8 @@ class EnvState(ctypes.Structure):
                 ("exit_count", vp), ("exit_y", vp), ("exit_x", vp),
                 ("level_index", vp), ("episodes", vp), ("num_steps", vp),
                 ("spawn_flags", vp), ("start_roll", vp), ("planes", vp), ("planes_ok", vp),
-                ("elig_planes", vp), ("board_planes", vp), ("board_zero", u32)]
+                ("elig_planes", vp), ("board_planes", vp), ("board_zero", u32),
+                ("planes_live", i32)]
 
 
 class LevelPool(ctypes.Structure):

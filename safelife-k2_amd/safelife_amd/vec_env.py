@@ -57,6 +57,18 @@ def _sched(val, counter):
     return val(counter.num_steps) if callable(val) else val
 
 
+def zero_planes(bits, can_toggle_powers=False, can_toggle_colors=False):
+    """sl_env_state.board_zero for boards holding cell bits `bits`: the bits none of them
+    can ever hold -- not set by a birth or a spawn (LIFE; colours only where present), an
+    exit (COLOR_R) or a toggle (powers / colours when those can be toggled)."""
+    can = bits | 0x0009 | 0x0200
+    if can_toggle_powers:
+        can |= 0x00E1
+    if can_toggle_colors:
+        can |= 0x0E00
+    return (~can) & 0xFFFF
+
+
 def start_board_hi_bits(start_board):
     """Per env: does any start-board cell use bits 12-14 (used by no cell type)?"""
     import torch
@@ -247,15 +259,8 @@ class SafeLifeVecEnv:
         return int(np.bitwise_or.reduce(pool.board.reshape(-1))) if pool.board.size else 0
 
     def _zero_planes(self, bits):
-        """sl_env_state.board_zero: the cell bits no board of this batch can hold -- none
-        in its boards (`bits`), not set by a birth or a spawn (LIFE, colours present), an
-        exit (COLOR_R) or a toggle (powers / colours when they can be toggled)."""
-        can = bits | 0x0009 | 0x0200
-        if self.can_toggle_powers:
-            can |= 0x00E1
-        if self.can_toggle_colors:
-            can |= 0x0E00
-        return (~can) & 0xFFFF
+        """sl_env_state.board_zero of this batch for boards with cell bits `bits`."""
+        return zero_planes(bits, self.can_toggle_powers, self.can_toggle_colors)
 
     def _allow_board_bits(self, bits):
         """Boards with cell bits `bits` are about to enter the batch: planes that must now
@@ -270,6 +275,7 @@ class SafeLifeVecEnv:
             self.sync_board()
             self.planes_ok.bitwise_and_(~(64 | 128))
             s.board_zero = new
+            s.planes_live = 0
 
     def _device_board_bits(self, boards):
         """OR of every cell of a uint16 device tensor (16 reductions; rare events only)."""
@@ -645,6 +651,7 @@ class SafeLifeVecEnv:
                                           fr["act_d"].data_ptr(), ctypes.byref(cfg),
                                           *[o.data_ptr() for o in outs],
                                           _lib.stream_ptr(self.device)), "sl_env_step")
+        self._state.planes_live |= st.planes_live     # (the slice may have left planes)
         if self.stream_error_of(sc, 1):
             raise RuntimeError("reference step consumed more draws than staged")
         speedups._buffer.take(int(fr["pos"].item()))
@@ -732,8 +739,8 @@ class SafeLifeVecEnv:
         s.B, s.H, s.W = n, self.H, self.W
         for name, _ in _lib.EnvState._fields_[3:]:
             base = getattr(full, name)
-            if name == "board_zero":          # (a mask, not a per-env pointer)
-                s.board_zero = base
+            if name in ("board_zero", "planes_live"):     # (not per-env pointers)
+                setattr(s, name, base)
                 continue
             if not base:
                 setattr(s, name, None)
