@@ -118,17 +118,23 @@ __device__ __forceinline__ void read_pairs(const lds_u32 *buf, int lane, u32 D[3
 // the board has been read out of it, so their (queueing-dominated) latency runs
 // under the action and the rule (issued at scoring time, it was ~40% of a wave's
 // life; held in registers instead, it spills).
+// KEEP: the planes any board (and so any start board) can hold; a row whose two planes
+// the scores do not need (1, 3, 6 are never read) or no board holds is not copied
+template <u32 KEEP = 0xFFFFu>
 __device__ __forceinline__ void pool_dma(const sl_level_pool &pool, int li, lds_u32 *buf,
                                          int lane) {
     const char *pl = reinterpret_cast<const char *>(pool.board_planes + (int64_t)li * 16 * N);
+    constexpr u32 need = KEEP & 0xFF85u;         // planes 0, 2, 7-15
 #pragma unroll
     for (int k = 0; k < 7; k++) {       // LDS row k <- planes (0,1), (2,3), (6,7) .. (14,15)
         const int p0 = k < 2 ? 2 * k : 2 * k + 2;
+        if (!((need >> p0) & 3u)) continue;
         __builtin_amdgcn_global_load_lds((const void *)(pl + p0 * N * 8 + lane * 16),
                                          (__attribute__((address_space(3))) void *)(buf + k * 256),
                                          16, 0, 0);
     }
 }
+template <u32 KEEP = 0xFFFFu>
 __device__ __forceinline__ void pool_planes_lds(const lds_u32 *buf, int dy, int dx, int lane,
                                                 u32 S[32]) {
     const int c0 = (2 * (lane >> 1) - dx) & 63, c1 = (c0 + 1) & 63;
@@ -137,7 +143,7 @@ __device__ __forceinline__ void pool_planes_lds(const lds_u32 *buf, int dy, int 
     const u32 sh = (u32)(r & 31);
 #pragma unroll
     for (int p = 0; p < 16; p++) {
-        if (p == 1 || (p >= 3 && p <= 6)) {
+        if (p == 1 || (p >= 3 && p <= 6) || !((KEEP >> p) & 1u)) {
             PL(S, p, 0) = 0u;
             PL(S, p, 1) = 0u;
             continue;
@@ -896,7 +902,10 @@ __device__ __forceinline__ u32 lds_plane_cell(const lds_u32 *buf, PlaneSlots<K16
     return v;
 }
 
-template <u32 K16>
+// OBS: 1 also writes the packed views (write_obs) from the step's planes: the goal
+// colours added into planes 12-14 (a bit-sliced adder, exact whatever the board's bits),
+// ONE transpose, the view-form rows into the buffer
+template <u32 K16, int OBS>
 __global__ void __launch_bounds__(64, kMinWaves)
 k_env_step_bits64_planes(StepKArgs ka) {
     const sl_env_state &st = ka.st;
@@ -1029,8 +1038,9 @@ k_env_step_bits64_planes(StepKArgs ka) {
 #pragma unroll
     for (int q = 0; q < 32; q++) PB[q] = ps.kept(q) ? buf[ps.pos(q) * 64 + lane] : 0u;
     wait_lgkm();
+    constexpr u32 KEEP = K16 ? K16 : 0xFFFFu;
     if (roll < 0) dma_board(st.start_board + off, buf, lane);
-    else pool_dma(fx.pool, rec(V, R_LI), buf, lane);
+    else pool_dma<KEEP>(fx.pool, rec(V, R_LI), buf, lane);
     (void)mux_edits(PB, ne, eidx, eval, lane);
     // held: changed cells that held a plane a change clears but never sets
     u32 cb[2], held[2];
@@ -1044,7 +1054,7 @@ k_env_step_bits64_planes(StepKArgs ka) {
     u32 PS[32];
     wait_vm();
     if (roll >= 0) {
-        pool_planes_lds(buf, roll >> 16, roll & 0xFFFF, lane, PS);
+        pool_planes_lds<KEEP>(buf, roll >> 16, roll & 0xFFFF, lane, PS);
     } else {
         read_pairs(buf, lane, PS);
         transpose32(PS);
@@ -1099,6 +1109,36 @@ k_env_step_bits64_planes(StepKArgs ka) {
     }
     const int ok = gok | kPok64Board;
     if (ok != pok_all && lane == 0) st.planes_ok[b] = ok;
+    if (OBS) {
+        const bool rw = kernarg().fx.obs_rw != 0;
+#pragma unroll
+        for (int w = 0; w < 2; w++) {
+            u32 g0 = gcol[0][w], g1 = gcol[1][w], g2 = gcol[2][w];
+            if (rw) {                                // white goals are background
+                const u32 wh = g0 & g1 & g2;
+                g0 &= ~wh;
+                g1 &= ~wh;
+                g2 &= ~wh;
+            }
+            const u32 b12 = PL(PB, 12, w), b13 = PL(PB, 13, w), b14 = PL(PB, 14, w);
+            u32 c = b12 & g0;
+            PL(PB, 12, w) = b12 ^ g0;
+            const u32 x13 = b13 ^ g1;
+            PL(PB, 13, w) = x13 ^ c;
+            c = (b13 & g1) | (c & x13);
+            const u32 x14 = b14 ^ g2;
+            PL(PB, 14, w) = x14 ^ c;
+            c = (b14 & g2) | (c & x14);
+            PL(PB, 15, w) ^= c;                      // (the carry out of bit 15 drops)
+        }
+        transpose32(PB);
+        lds_put_board(buf, lane, PB);               // (the start planes have been read)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        write_obs(buf, fx, fl, b, lane);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     int reset = 0;
     if (lane == 0)
         reset = epilogue_core(st, a, b, fl, act_reward, points, score, possible, side_total,
@@ -1282,12 +1322,20 @@ int launch_step_bits(const sl_env_state &st, const StepArgs &a, const FastExtra 
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
         if (fx.plane_mode) {
             const u32 keep = ~st.board_zero & 0xFFFFu;
-            if (keep == kKeepC3)
-                hipLaunchKernelGGL(k_env_step_bits64_planes<kKeepC3>, dim3(grid), dim3(64), 0, s, ka);
-            else if (keep == kKeepAll)
-                hipLaunchKernelGGL(k_env_step_bits64_planes<kKeepAll>, dim3(grid), dim3(64), 0, s, ka);
-            else
-                hipLaunchKernelGGL(k_env_step_bits64_planes<0>, dim3(grid), dim3(64), 0, s, ka);
+            if (fx.obs_out) {
+                if (keep == kKeepC3)
+                    hipLaunchKernelGGL((k_env_step_bits64_planes<kKeepC3, 1>), dim3(grid), dim3(64), 0, s, ka);
+                else if (keep == kKeepAll)
+                    hipLaunchKernelGGL((k_env_step_bits64_planes<kKeepAll, 1>), dim3(grid), dim3(64), 0, s, ka);
+                else
+                    hipLaunchKernelGGL((k_env_step_bits64_planes<0, 1>), dim3(grid), dim3(64), 0, s, ka);
+            } else if (keep == kKeepC3) {
+                hipLaunchKernelGGL((k_env_step_bits64_planes<kKeepC3, 0>), dim3(grid), dim3(64), 0, s, ka);
+            } else if (keep == kKeepAll) {
+                hipLaunchKernelGGL((k_env_step_bits64_planes<kKeepAll, 0>), dim3(grid), dim3(64), 0, s, ka);
+            } else {
+                hipLaunchKernelGGL((k_env_step_bits64_planes<0, 0>), dim3(grid), dim3(64), 0, s, ka);
+            }
         }
         else
             launch_bits64<SPAWN_PHILOX>(obs_kind(fx), grid, ka, s);

@@ -1060,9 +1060,10 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
                      (!replay || st->elig_planes) && cfg->board_mode != SL_BOARD_UINT16) ? 1 : 0;
     // 64x64: a Philox step without views or capture (sl_bits.hip, plane mode)
     const bool planes64 = planes64_shape(*st);
-    if (planes64)
-        fx.plane_mode = (fast && !cfg->obs_out && !cap && !replay &&
-                         cfg->board_mode != SL_BOARD_UINT16) ? 1 : 0;
+    if (planes64)       // (packed views: written from the planes, fused_obs64 below)
+        fx.plane_mode = (fast && !cap && !replay && cfg->board_mode != SL_BOARD_UINT16 &&
+                         (!cfg->obs_out || (oa.mode == SL_OBS_PACKED &&
+                                            oa.vh * oa.vw <= kObsMaxCells))) ? 1 : 0;
     if ((planes128 || planes64) && !fx.plane_mode) {
         const int rc = demote_planes(st, s);
         if (rc) return rc;

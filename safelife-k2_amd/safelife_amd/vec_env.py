@@ -807,7 +807,8 @@ class SafeLifeVecEnv:
         mirrors are stale and the reset lists start empty."""
         self.st_t["start_roll"].fill_(-1)
         if self._state.board_zero:      # boards written from outside: their bits count
-            self._state.board_zero &= self._zero_planes(self._device_board_bits(self._board))
+            self._state.board_zero &= self._zero_planes(self._device_board_bits(self._board)
+                                                        | self._device_board_bits(self.start_board))
         # may hold spawners (replay counts them); bit 2 (128x128 boards): the start board
         # uses cell bits 12-14, which the 128x128 kernel then compares in a second pass
         hi = start_board_hi_bits(self.start_board) & ((self.H, self.W) == (128, 128))

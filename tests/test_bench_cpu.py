@@ -41,12 +41,15 @@ def test_labels():
     assert "25×25" in bench.metric_name(25, 25, 4096)
     # the 64x64 board in bit planes (round 6): the instance for the planes the pool keeps
     assert (bench.step_kernel_name(64, 64, "none", "auto", keep=0x877F)
-            == "k_env_step_bits64_planes<34687u>")
+            == "k_env_step_bits64_planes<34687u, 0>")
     assert (bench.step_kernel_name(64, 64, "none", "auto", keep=0x1234)
-            == "k_env_step_bits64_planes<0u>")
+            == "k_env_step_bits64_planes<0u, 0>")
     assert (bench.step_kernel_name(64, 64, "none", "auto", planes=False)
             == "k_env_step_bits64<0, 0>")
-    assert bench.step_kernel_name(64, 64, "packed", "auto") == "k_env_step_bits64<1, 0>"
+    assert (bench.step_kernel_name(64, 64, "packed", "auto", keep=0x877F)
+            == "k_env_step_bits64_planes<34687u, 1>")
+    assert (bench.step_kernel_name(64, 64, "packed", "auto", planes=False)
+            == "k_env_step_bits64<1, 0>")
     assert bench.step_kernel_name(25, 25, "none", "auto") == "k_env_step_seg4<0, true>"
     assert bench.step_kernel_name(25, 29, "none", "auto") == "k_env_step_seg4<0, false>"
     assert bench.step_kernel_name(25, 40, "none", "auto") == "k_env_step_small<0>"
@@ -57,7 +60,7 @@ def test_labels():
             == "k_env_step_bits64<0, 1>")
     # replay without any spawner runs the Philox form (in planes)
     assert (bench.step_kernel_name(64, 64, "none", "auto", "stream", replay=False,
-                                   keep=0xFFFF) == "k_env_step_bits64_planes<65535u>")
+                                   keep=0xFFFF) == "k_env_step_bits64_planes<65535u, 0>")
     assert bench.step_kernel_name(64, 64, "none", "generic") == "k_env_step_generic"
     # channel views are written by the step kernel (obs_kind 2: u16 / bf16, 3: u8, 4: f32)
     assert bench.step_kernel_name(64, 64, "channels", "auto") == "k_env_step_bits64<2, 0>"
