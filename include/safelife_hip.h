@@ -393,7 +393,7 @@ typedef struct sl_env_state {
                                  the board's planes in half 0 of the goals
                                  mirror (Philox steps without views; bit 7
                                  only after a sync or a reset).                */
-    uint32_t board_zero;      /* 64x64 plane mode: cell bits (planes) that are
+    uint32_t board_zero;      /* plane mode (64x64, 128x128): cell bits (planes) that are
                                  0 in every board of the batch and that no rule,
                                  action or reset can set (the caller's promise:
                                  none in its levels or written boards, not

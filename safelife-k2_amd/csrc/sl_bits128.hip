@@ -442,7 +442,13 @@ __device__ __forceinline__ void view_exits_store(const ViewExit &ve, int64_t b, 
 // overlay.  MODE: SPAWN_PHILOX; SPAWN_STREAM (each tensor's first uniform from the
 // scratch offsets); or SPAWN_DECIDED (the spawns from the draw planes k_stream_draw128
 // left, replay with sl_env_state.elig_planes).
-template <int MODE, bool VIEW>
+// KEEP: the board planes any board of the batch can hold (sl_env_state.board_zero's
+// complement, or a superset of it): the others are neither loaded nor stored in plane
+// mode.  Instantiated for every plane and for the C5 levels' (cell bits 0, 1, 3-10:
+// 10 of 16 planes, 37 % fewer plane bytes)
+constexpr u32 kKeep128All = 0xFFFFu, kKeep128C5 = 0x07FBu;
+
+template <int MODE, bool VIEW, u32 KEEP>
 __device__ __forceinline__ void step128_body(const Step128KArgs &ka) {
     const sl_env_state &st = ka.st;
     const StepArgs &a = ka.a;
@@ -617,8 +623,8 @@ __device__ __forceinline__ void step128_body(const Step128KArgs &ka) {
 #pragma unroll
             for (int k = 0; k < 32; k++) {
                 const int pl = k & 15;
-                P[k] = (lo12 && pl >= 12 && pl <= 14) ? 0u
-                                                      : __builtin_nontemporal_load(&bpl[t * MW + k * 64]);
+                P[k] = ((lo12 && pl >= 12 && pl <= 14) || !((KEEP >> pl) & 1u))
+                           ? 0u : __builtin_nontemporal_load(&bpl[t * MW + k * 64]);
             }
             last = gb[(32 * t + 31) * RS];     // (this band's edge store comes after)
         } else {
@@ -723,16 +729,18 @@ __device__ __forceinline__ void step128_body(const Step128KArgs &ka) {
 #pragma unroll
                 for (int w = 0; w < 2; w++) {
                     __builtin_nontemporal_store(PL(P, 0, w), &bpl[t * MW + (0 + 16 * w) * 64]);
-                    __builtin_nontemporal_store(PL(P, 3, w), &bpl[t * MW + (3 + 16 * w) * 64]);
+                    if ((KEEP >> 3) & 1u)
+                        __builtin_nontemporal_store(PL(P, 3, w), &bpl[t * MW + (3 + 16 * w) * 64]);
 #pragma unroll
                     for (int k = 9; k <= 11; k++)
-                        __builtin_nontemporal_store(PL(P, k, w), &bpl[t * MW + (k + 16 * w) * 64]);
+                        if ((KEEP >> k) & 1u)
+                            __builtin_nontemporal_store(PL(P, k, w), &bpl[t * MW + (k + 16 * w) * 64]);
                 }
                 if (wave_or((oth[0] & cb[0]) | (oth[1] & cb[1]))) {
 #pragma unroll
                     for (int k = 0; k < 32; k++) {
                         const int pl = k & 15;
-                        if (pl != 0 && pl != 3 && (pl < 9 || pl > 11))
+                        if (pl != 0 && pl != 3 && (pl < 9 || pl > 11) && ((KEEP >> pl) & 1u))
                             __builtin_nontemporal_store(P[k], &bpl[t * MW + k * 64]);
                     }
                 }
@@ -754,7 +762,7 @@ __device__ __forceinline__ void step128_body(const Step128KArgs &ka) {
                 const u32 pkw = wave_or(pk);
 #pragma unroll
                 for (int k = 0; k < 32; k++)
-                    if ((pkw >> k) & 1u)
+                    if (((KEEP >> (k & 15)) & 1u) && ((pkw >> k) & 1u))
                         if ((pk >> k) & 1u) bpl[t * MW + k * 64] = P[k];
             }
             // the cells the next action can read (changed or not: they may be stale
@@ -785,7 +793,9 @@ __device__ __forceinline__ void step128_body(const Step128KArgs &ka) {
         } else {
             if (pmode) {        // into plane mode: every plane word, and the rows below
 #pragma unroll
-                for (int k = 0; k < 32; k++) __builtin_nontemporal_store(P[k], &bpl[t * MW + k * 64]);
+                for (int k = 0; k < 32; k++)
+                    if ((KEEP >> (k & 15)) & 1u)
+                        __builtin_nontemporal_store(P[k], &bpl[t * MW + k * 64]);
                 if (MODE == SPAWN_DECIDED) {
 #pragma unroll
                     for (int w = 0; w < 2; w++) hi12 |= PL(P, 12, w) | PL(P, 13, w) | PL(P, 14, w);
@@ -852,17 +862,33 @@ __device__ __forceinline__ void step128_body(const Step128KArgs &ka) {
 }
 
 // the step kernel: Philox, the stream fallback or decided replay; no views
-template <int MODE>
+template <int MODE, u32 KEEP>
 __global__ void __launch_bounds__(64, MODE == SPAWN_STREAM ? kMinWavesStream : kMinWaves)
 k_env_step_bits128(Step128KArgs ka) {
-    step128_body<MODE, false>(ka);
+    step128_body<MODE, false, KEEP>(ka);
 }
 
 // ... with packed views written from the planes (plane mode, fx.obs_out)
-template <int MODE>
+template <int MODE, u32 KEEP>
 __global__ void __launch_bounds__(64, kMinWaves)
 k_env_step_bits128_view(Step128KArgs ka) {
-    step128_body<MODE, true>(ka);
+    step128_body<MODE, true, KEEP>(ka);
+}
+
+// the instance for a plane-mode launch: the C5 planes when no board can hold another
+template <int MODE>
+void launch_step128(const Step128KArgs &ka, bool view, hipStream_t s) {
+    const dim3 grid((unsigned)ka.st.B);
+    const u32 keep = ~ka.st.board_zero & 0xFFFFu;
+    const bool c5 = ka.fx.plane_mode && !(keep & ~kKeep128C5);
+    if (view && c5)
+        hipLaunchKernelGGL((k_env_step_bits128_view<MODE, kKeep128C5>), grid, dim3(64), 0, s, ka);
+    else if (view)
+        hipLaunchKernelGGL((k_env_step_bits128_view<MODE, kKeep128All>), grid, dim3(64), 0, s, ka);
+    else if (c5)
+        hipLaunchKernelGGL((k_env_step_bits128<MODE, kKeep128C5>), grid, dim3(64), 0, s, ka);
+    else
+        hipLaunchKernelGGL((k_env_step_bits128<MODE, kKeep128All>), grid, dim3(64), 0, s, ka);
 }
 
 // Replay-mode count of env b (SL_RNG_STREAM), one wave, after k_env_action (one lane
@@ -901,7 +927,9 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
     // put into them here, for this count and for the step kernel
     const bool pm = ka.fx.plane_mode && st.board_planes && (rec(V, R_POK) & 64);
     u32 *const bpw = pm ? st.board_planes + b * (int64_t)(NB * MW) : nullptr;
-    auto pload = [&](int t, int k) {       // (past the vector L1: the edits just stored)
+    const u32 zero = st.board_zero;          // planes no board holds (never stored)
+    auto pload = [&](int t, int k) -> u32 {  // (past the vector L1: the edits just stored)
+        if ((zero >> (k & 15)) & 1u) return 0u;
         return __hip_atomic_load(bpw + t * MW + k * 64 + lane, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
     };
@@ -911,7 +939,7 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
         for (int m = 0; m < 4; m++) {
             const int i = (int)((ec >> (16 * m)) & 0xFFFFu);
             if (i >= N * N) continue;
-            if (lane < 16) {                 // lane p: plane p
+            if (lane < 16 && !((zero >> lane) & 1u)) {     // lane p: plane p
                 const u32 v = st.board[off + i];
                 const int x = i & (N - 1);
                 const u32 bit = 1u << ((i >> 7) & 31);
@@ -1395,11 +1423,12 @@ __global__ void __launch_bounds__(64) k_board_sync128(sl_env_state st, int demot
         wait_vm();
         const u32 *bp = st.board_planes + b * (int64_t)(NB * MW) + lane;
         u32 *gb = reinterpret_cast<u32 *>(st.board + b * (int64_t)(N * N)) + lane;
+        const u32 zero = st.board_zero;     // (planes no board holds: never stored)
 #pragma unroll 1
         for (int t = 0; t < NB; t++) {
             u32 P[32];
 #pragma unroll
-            for (int k = 0; k < 32; k++) P[k] = bp[t * MW + k * 64];
+            for (int k = 0; k < 32; k++) P[k] = ((zero >> (k & 15)) & 1u) ? 0u : bp[t * MW + k * 64];
             transpose32(P);
 #pragma unroll
             for (int y = 0; y < 32; y++) gb[(32 * t + y) * RS] = P[y];
@@ -1454,13 +1483,10 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
                 hipLaunchKernelGGL(k_stream_draw128, grid, dim3(64), 0, s, ka);
             if (hipGetLastError() != hipSuccess) return SL_EHIP;
             if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-            if (fx.plane_mode && fx.obs_out)
-                hipLaunchKernelGGL(k_env_step_bits128_view<SPAWN_DECIDED>, grid, dim3(64), 0, s, ka);
-            else
-                hipLaunchKernelGGL(k_env_step_bits128<SPAWN_DECIDED>, grid, dim3(64), 0, s, ka);
+            launch_step128<SPAWN_DECIDED>(ka, fx.plane_mode && fx.obs_out, s);
         } else {
             if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-            hipLaunchKernelGGL(k_env_step_bits128<SPAWN_STREAM>, grid, dim3(64), 0, s, ka);
+            hipLaunchKernelGGL((k_env_step_bits128<SPAWN_STREAM, kKeep128All>), grid, dim3(64), 0, s, ka);
         }
     } else {
         if (fx.plane_mode) {
@@ -1473,10 +1499,7 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
             if (rc) return rc;
         }
         if (fx.ev_begin) (void)hipEventRecord((hipEvent_t)fx.ev_begin, s);
-        if (fx.plane_mode && fx.obs_out)
-            hipLaunchKernelGGL(k_env_step_bits128_view<SPAWN_PHILOX>, grid, dim3(64), 0, s, ka);
-        else
-            hipLaunchKernelGGL(k_env_step_bits128<SPAWN_PHILOX>, grid, dim3(64), 0, s, ka);
+        launch_step128<SPAWN_PHILOX>(ka, fx.plane_mode && fx.obs_out, s);
     }
     if (hipGetLastError() != hipSuccess) return SL_EHIP;
     if (fx.ev_end) (void)hipEventRecord((hipEvent_t)fx.ev_end, s);

@@ -217,10 +217,11 @@ class SafeLifeVecEnv:
             s.board_zero = self._zero_planes(self._pool_bits(self.pool))
         if (H, W) == (128, 128):
             # the 128x128 board in bit planes, kept there by steps without observations
-            # (sl_env_state.board_planes); `board` completes the uint16 tensor when it
-            # is read
+            # or with packed views (sl_env_state.board_planes); `board` completes the
+            # uint16 tensor when it is read
             self.board_planes = z(B, H // 32, 32, 64)
             s.board_planes = self.board_planes.data_ptr()
+            s.board_zero = self._zero_planes(self._pool_bits(self.pool))
         if (H, W) == (128, 128) and self.rng == "stream":
             # replay's draw planes: each tensor's eligible cells, then its decided
             # spawns (4 KiB per env)

@@ -53,9 +53,14 @@ def test_labels():
     assert bench.step_kernel_name(25, 25, "none", "auto") == "k_env_step_seg4<0, true>"
     assert bench.step_kernel_name(25, 29, "none", "auto") == "k_env_step_seg4<0, false>"
     assert bench.step_kernel_name(25, 40, "none", "auto") == "k_env_step_small<0>"
-    assert bench.step_kernel_name(128, 128, "none", "auto") == "k_env_step_bits128<0>"
-    assert (bench.step_kernel_name(128, 128, "none", "auto", "stream")
-            == "k_env_step_bits128<3>")                  # draws decided before the step
+    assert (bench.step_kernel_name(128, 128, "none", "auto", keep=0x07FB)
+            == "k_env_step_bits128<0, 2043u>")         # the C5 planes' instance
+    assert (bench.step_kernel_name(128, 128, "none", "auto", keep=0xFFFF)
+            == "k_env_step_bits128<0, 65535u>")
+    assert (bench.step_kernel_name(128, 128, "none", "auto", "stream", keep=0x07FB)
+            == "k_env_step_bits128<3, 2043u>")         # draws decided before the step
+    assert (bench.step_kernel_name(128, 128, "packed", "auto", keep=0x07FB)
+            == "k_env_step_bits128_view<0, 2043u>")
     assert (bench.step_kernel_name(64, 64, "none", "auto", "stream")
             == "k_env_step_bits64<0, 1>")
     # replay without any spawner runs the Philox form (in planes)
@@ -108,7 +113,8 @@ def test_cache_resident_configs_claim_no_hbm_fraction():
 def test_seeded_replay_names():
     """--rng seeded runs the replay kernels with the device generator; its PMC record
     is its own."""
-    assert bench.step_kernel_name(128, 128, "none", "auto", "seeded") == "k_env_step_bits128<3>"
+    assert (bench.step_kernel_name(128, 128, "none", "auto", "seeded", keep=0x07FB)
+            == "k_env_step_bits128<3, 2043u>")
     assert bench.pmc_record_path("c5", "none", "seeded").endswith("pmc_c5_seeded.json")
     assert bench.pmc_record_path("c5", "none", "stream").endswith("pmc_c5_stream.json")
 
