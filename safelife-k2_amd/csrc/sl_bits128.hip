@@ -933,23 +933,24 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
         return __hip_atomic_load(bpw + t * MW + k * 64 + lane, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
     };
-    if (pm) {
-        const uint64_t ec = (uint64_t)w.act[3 * st.B + b];
-#pragma unroll 1
-        for (int m = 0; m < 4; m++) {
-            const int i = (int)((ec >> (16 * m)) & 0xFFFFu);
-            if (i >= N * N) continue;
-            if (lane < 16 && !((zero >> lane) & 1u)) {     // lane p: plane p
-                const u32 v = st.board[off + i];
-                const int x = i & (N - 1);
-                const u32 bit = 1u << ((i >> 7) & 31);
-                u32 *wd = bpw + (i >> 12) * MW + (lane + 16 * (x & 1)) * 64 + (x >> 1);
-                const u32 o = __hip_atomic_load(wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                *wd = ((v >> lane) & 1u) ? o | bit : o & ~bit;
-            }
-            wait_vm();
-        }
-    }
+    // the action's edited cells (act[3B + b], up to four 16-bit indices): lane 16 m + p
+    // holds edit m's new cell value and puts its plane p into the planes (put_edits, an
+    // OR or an AND of the cell's bit, nothing waited for); count_next patches its
+    // window's words in registers, so the edits cost one load in flight with the others
+    const uint64_t ec = pm ? (uint64_t)w.act[3 * st.B + b] : ~0ull;
+    const int ei = (int)((ec >> (16 * (lane >> 4))) & 0xFFFFu);
+    const u32 ev = (pm && ei < N * N) ? (u32)st.board[off + ei] : 0u;
+    auto put_edits = [&]() {
+        const int pl = lane & 15;
+        if (!pm || ei >= N * N || ((zero >> pl) & 1u)) return;
+        const int x = ei & (N - 1);
+        const u32 bit = 1u << ((ei >> 7) & 31);
+        u32 *wd = bpw + (ei >> 12) * MW + (pl + 16 * (x & 1)) * 64 + (x >> 1);
+        if ((ev >> pl) & 1u)
+            __hip_atomic_fetch_or(wd, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            __hip_atomic_fetch_and(wd, ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     auto keep = [&](const GeoBand<SPAWN_COUNT> &geo, int tensor, int t) {
         if (dp) {
             dp[(tensor * NB + t) * 128] = geo.e[0];
@@ -1030,6 +1031,28 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
                     P[k] = (sh ? __builtin_amdgcn_alignbit(hi, lo, sh) : lo) & nm;
                 }
             }
+            // the edits, into the window's words (the planes in HBM get them after)
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                const int i = (int)((ec >> (16 * m)) & 0xFFFFu);
+                if (i >= N * N) continue;                           // wave-uniform
+                const int r = ((i >> 7) - base) & (N - 1), x = i & (N - 1);
+                if (r >= nrows) continue;
+                const u32 v = (u32)__builtin_amdgcn_readlane((int)ev, 16 * m);
+                const u32 bit = 1u << r;
+                const bool mine = lane == (x >> 1);
+                if (x & 1) {
+                    PL(P, 0, 1) = mine ? ((v & 1u) ? PL(P, 0, 1) | bit : PL(P, 0, 1) & ~bit) : PL(P, 0, 1);
+                    PL(P, 4, 1) = mine ? ((v & 16u) ? PL(P, 4, 1) | bit : PL(P, 4, 1) & ~bit) : PL(P, 4, 1);
+                    PL(P, 6, 1) = mine ? ((v & 64u) ? PL(P, 6, 1) | bit : PL(P, 6, 1) & ~bit) : PL(P, 6, 1);
+                    PL(P, 7, 1) = mine ? ((v & 128u) ? PL(P, 7, 1) | bit : PL(P, 7, 1) & ~bit) : PL(P, 7, 1);
+                } else {
+                    PL(P, 0, 0) = mine ? ((v & 1u) ? PL(P, 0, 0) | bit : PL(P, 0, 0) & ~bit) : PL(P, 0, 0);
+                    PL(P, 4, 0) = mine ? ((v & 16u) ? PL(P, 4, 0) | bit : PL(P, 4, 0) & ~bit) : PL(P, 4, 0);
+                    PL(P, 6, 0) = mine ? ((v & 64u) ? PL(P, 6, 0) | bit : PL(P, 6, 0) & ~bit) : PL(P, 6, 0);
+                    PL(P, 7, 0) = mine ? ((v & 128u) ? PL(P, 7, 0) | bit : PL(P, 7, 0) & ~bit) : PL(P, 7, 0);
+                }
+            }
         } else {
 #pragma unroll
             for (int i = 0; i < 32; i++) P[i] = i < nrows ? gb[((base + i) & (N - 1)) * RS] : 0u;
@@ -1068,10 +1091,17 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
     const int spf = rec(V, R_SPF) | (ka.ctp ? 1 : 0);     // toggling powers can make one
     const bool next = st.elig_planes && (rec(V, R_POK) & 8);
     int nb = 0;
+    bool put = false;
     if (spf & 1) {
         nb = next ? count_next() : -1;
-        if (nb < 0) nb = count(gb, 0);
+        if (nb < 0) {                   // the whole count reads the planes: edits first
+            put_edits();
+            put = true;
+            wait_vm();
+            nb = count(gb, 0);
+        }
     }
+    if (!put) put_edits();
     const int ng = ((rec(V, R_POK) & 6) == 6 || !(spf & 2)) ? 0 : count(gg, 1);
     const int dfl = (nb ? 1 : 0) | (ng ? 2 : 0);
     if (lane == 0) {
@@ -1323,18 +1353,18 @@ k_stream_draw128_bits(Step128KArgs ka) {
             const int sh = (int)(at[t] & 31);
             uint64_t sb = ((((uint64_t)w1[t]) << 32) | w0[t]) >> sh;
             if (sh) sb |= ((uint64_t)w2[t]) << (64 - sh);
-            u32 m = R0[t] | R1[t], s0 = 0u, s1 = 0u;
+            // column pair i in order: the even column's cell (e) takes the next bit,
+            // the odd one's (f) the bit after it when e is set -- branch-free, 12 VALU
+            // a pair instead of 21 (the loop runs to the wave's fullest segment)
+            const u32 r0 = R0[t], r1 = R1[t];
+            u32 m = r0 | r1, s0 = 0u, s1 = 0u;
             while (m) {
                 const int i = __builtin_ctz(m);
                 m &= m - 1u;
-                if ((R0[t] >> i) & 1u) {
-                    s0 |= (u32)(sb & 1u) << i;
-                    sb >>= 1;
-                }
-                if ((R1[t] >> i) & 1u) {
-                    s1 |= (u32)(sb & 1u) << i;
-                    sb >>= 1;
-                }
+                const u32 e = (r0 >> i) & 1u, f = (r1 >> i) & 1u, lo = (u32)sb;
+                s0 |= (lo & e) << i;
+                s1 |= ((lo >> e) & f) << i;
+                sb >>= e + f;
             }
             // back to the planes' layout (transpose_halves is an involution)
             dp[(tensor * NB + t) * 128] = transpose_halves(s0, lane) & E[t][0];
