@@ -1107,6 +1107,9 @@ __device__ __forceinline__ void count_env128(const Step128KArgs &ka, int64_t b, 
     if (lane == 0) {
         w.counts[2 * b] = nb;
         w.counts[2 * b + 1] = ng;
+        // the bit ring serves only envs with its threshold (k_bits_thr_check's test)
+        if (ka.fx.bits_thr >= 0.0 && (nb | ng) && (double)st.spawn_prob[b] != ka.fx.bits_thr)
+            atomicOr((unsigned long long *)w.err, (unsigned long long)SL_STREAM_ERR_THRESHOLD);
         // the tensors that draw, for the draws and the step (the action's edited rows
         // in this slot have been read)
         if (dp) w.act[st.B + b] = dfl;
@@ -1504,7 +1507,9 @@ int launch_step_bits128(const sl_env_state &st, const StepArgs &a, const FastExt
             hipLaunchKernelGGL(k_stream_prologue128, grid, dim3(64), 0, s, ka);
             if (hipGetLastError() != hipSuccess) return SL_EHIP;
         }
-        const int rc = stream_offsets(st, fx, s);
+        FastExtra fo = fx;
+        fo.thr_checked = stream_counts(fx);     // (in the count prologue)
+        const int rc = stream_offsets(st, fo, s);
         if (rc || !stream_steps(fx)) return rc;
         if (st.elig_planes) {       // draws decided up front
             if (a.draw_bits)

@@ -927,7 +927,7 @@ int sl::bits_thr_check(const sl_env_state &st, const sl_mt19937 *mt, const int64
 
 int sl::stream_offsets(const sl_env_state &st, const FastExtra &fx, hipStream_t s) {
     const Scratch sc = scratch_of(fx.scratch, st.B);
-    if (fx.mt && fx.stream_phase != 2) {
+    if (fx.mt && fx.stream_phase != 2 && !fx.thr_checked) {
         const int rcb = bits_thr_check(st, fx.mt, sc.counts, sc.err, s);
         if (rcb) return rcb;
     }
@@ -1033,6 +1033,7 @@ extern "C" int sl_env_step(sl_env_state *st, const sl_level_pool *pool, const in
     fx.stream_phase = cfg->stream_phase;
     fx.stream_base = cfg->stream_base;
     fx.mt = replay ? cfg->mt : nullptr;
+    if (fx.mt && fx.mt->bit_ring) fx.bits_thr = fx.mt->bits_thr;
     fx.ev_begin = cfg->ev_begin;
     // the small-board kernel resets finished envs inside the step; with a capture the
     // resets run in the follow-up scan so the pre-reset frame can be copied first.

@@ -347,6 +347,9 @@ struct FastExtra {
     const int64_t *stream_base;   // *stream_base + the step
     const sl_mt19937 *mt;   // replay from the device generator (sl_env_cfg.mt) or NULL:
                             // stream_offsets fills its ring for the step's range
+    double bits_thr = -1.0; // the device generator's bit ring: its threshold (else < 0);
+    int32_t thr_checked = 0;// the 128x128 count prologue checks it (stream_offsets then
+                            // launches no k_bits_thr_check)
     int32_t plane_mode = 0; // 128x128 step without capture (no views, or packed views of
                             // <= kViewMaxRows128 rows written from the planes; replay
                             // with draw planes), board_planes set: the board is kept in

@@ -143,6 +143,37 @@ def test_golden_trajectory_from_seed_alone(torch_dev, path, ring, kernel):
     assert not env.stream_error()
 
 
+@pytest.mark.parametrize("name", ["traj_nav128_c5.npz", "traj_prune_spawn_v10.npz"])
+def test_bit_ring_flags_a_foreign_threshold(torch_dev, name):
+    """A bit ring holds decisions for one threshold: an env that draws with another one
+    (spawn_prob written behind the env's back) sets SL_STREAM_ERR_THRESHOLD -- on 128x128
+    boards from the count prologue itself, elsewhere from k_bits_thr_check -- and the
+    poll raises; the flag stays clear while the threshold is the ring's."""
+    from safelife_amd import _lib
+    torch, dev = torch_dev
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", name))
+    env = _vec_env_from_traj(d, B=4, kernel="fast", spawn_stream=None, seed=int(d["cfg"][2]),
+                             stream_ring="auto")
+    assert env.mt is not None and env.mt.bits_threshold is not None
+    env.reset()
+    acts = torch.from_numpy(d["action"][:40].astype(np.int32)).to(dev)
+    for t in range(20):
+        env.step_async(acts[t].repeat(4))
+    assert not env.stream_error()
+    env.st_t["spawn_prob"][2] = 0.25          # (not through set_state: the ring is kept)
+    drew = False
+    for t in range(20, 40):
+        env.step_async(acts[t].repeat(4))
+        drew = drew or bool(env.scratch[2 * 2:2 * 2 + 2].sum().item())     # env 2's counts
+    flag = int(env.scratch[8 * env.B].item())
+    if drew:
+        assert flag & _lib.SL_STREAM_ERR_THRESHOLD, flag
+        with pytest.raises(RuntimeError, match="spawn threshold"):
+            env._raise_stream_error(flag)
+    else:
+        assert flag == 0
+
+
 class _NumpyStream:
     """RandomState(seed).random_sample, extended on demand (slices as torch tensors)."""
 
