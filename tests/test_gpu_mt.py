@@ -37,25 +37,30 @@ def _ring_slice(torch, mt, lo, hi):
                                                        (420, 64, 1 << 24, None),
                                                        (36, 16, 1 << 21, 0.3),
                                                        (1684, 8, 1 << 24, 0.3),
-                                                       (420, 64, 1 << 24, 0.30000001192092896)])
+                                                       (420, 64, 1 << 24, 0.30000001192092896),
+                                                       (33, None, 1 << 21, None),
+                                                       (36, None, 1 << 21, 0.3)])
 def test_fill_matches_numpy(torch_dev, rounds, n_chains, ring, bits, lookahead):
     """Consecutive ranges, as replay steps consume the stream: empty, single draws,
     block-sized and multi-block ranges, all equal to RandomState(s).random_sample --
     also with the look-ahead generating each next range's blocks on a second stream
     while the test reads (and rewrites its range tensor for) the current one.  A bit
-    ring holds draw < threshold for every draw."""
+    ring holds draw < threshold for every draw.  n_chains None: sized by
+    MT19937Stream (the chains cover the ring and a block), which with the look-ahead
+    puts the chains' jumps on their own stream (sl_mt19937.jump_stream)."""
     torch, dev = torch_dev
     from safelife_amd.mtstream import MT19937Stream
     mt = MT19937Stream(2024, dev, ring_draws=ring, n_chains=n_chains, rounds=rounds,
                        lookahead=lookahead, bits_threshold=bits)
     D = mt.block
+    n_chains = mt.n_chains
     ref = np.random.RandomState(2024).random_sample(6 * n_chains * D)
     if bits is not None:
         ref = ref < bits
     rng = np.random.RandomState(0)
     lohi = torch.zeros(2, dtype=torch.int64, device=dev)
     pos, n_fills = 0, 0
-    sizes = [0, 1, 7, D - 1, D, D + 1, 3 * D + 17, (n_chains - 2) * D]
+    sizes = [0, 1, 7, D - 1, D, D + 1, 3 * D + 17, min((n_chains - 2) * D, ring - 2 * D)]
     while pos + (n_chains - 1) * D < len(ref):
         n = int(sizes[rng.randint(len(sizes))])
         lohi[0], lohi[1] = pos, pos + n
